@@ -1,0 +1,156 @@
+"""Pin the oracle (oracle/omcts_oracle.c, oracle/resnet_ref.py) against vectors
+the reference itself produced (tests/golden/, see make_golden.py)."""
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import resnet_ref
+
+
+def u(x):
+    return int(np.int64(x).view(np.uint64))
+
+
+@pytest.fixture(scope="module")
+def bb(golden_dir):
+    return np.load(golden_dir / "bitboards.npz")
+
+
+def _pos(player, p1, p2, legal):
+    p = O.CPos()
+    p.player, p.p1, p.p2, p.legal, p.next_legal = player, p1, p2, legal, 0
+    return p
+
+
+def test_transform_table(bb):
+    tab = bb["transform_table"]
+    for t in range(8):
+        for a in range(65):
+            assert O.transform_action(a, t) == tab[t, a]
+
+
+def test_legal_moves_random_boards(bb):
+    for me, opp, legal in zip(bb["rnd_me"], bb["rnd_opp"], bb["rnd_legal"]):
+        assert O.get_legal_moves(u(me), u(opp)) == u(legal)
+
+
+def test_flips_random_boards(bb):
+    me, opp = bb["rnd_me"], bb["rnd_opp"]
+    for i, sq, fl in zip(bb["fl_index"], bb["fl_square"], bb["fl_flips"]):
+        assert O.get_flips(1 << (63 - int(sq)), u(me[i]), u(opp[i])) == u(fl)
+
+
+def test_games_positions_and_children(bb):
+    player, p1, p2, legal = bb["pos_player"], bb["pos_p1"], bb["pos_p2"], bb["pos_legal"]
+    init = O.initial_position()
+    assert (init.player, init.p1, init.p2, init.legal) == (player[0], u(p1[0]), u(p2[0]), u(legal[0]))
+    # next_legal is private in the reference; rebuild it the way position.h:351-357 sets it
+    for k, (par, a, fl, cp, c1, c2, cl) in enumerate(
+        zip(bb["ch_parent"], bb["ch_action"], bb["ch_flips"], bb["ch_player"], bb["ch_p1"],
+            bb["ch_p2"], bb["ch_legal"])
+    ):
+        pp = _pos(int(player[par]), u(p1[par]), u(p2[par]), u(legal[par]))
+        me, opp = (pp.p1, pp.p2) if pp.player == 1 else (pp.p2, pp.p1)
+        if pp.legal == 0:
+            pp.next_legal = O.get_legal_moves(opp, me)
+        else:
+            assert O.get_flips(1 << (63 - int(a)), me, opp) == u(fl)
+        c = O.apply_action(pp, int(a))
+        assert (c.player, c.p1, c.p2, c.legal) == (cp, u(c1), u(c2), u(cl)), k
+    for idx, val in zip(bb["lm_index"], bb["lm_value"]):
+        pl = int(player[idx])
+        me, opp = (u(p1[idx]), u(p2[idx])) if pl == 1 else (u(p2[idx]), u(p1[idx]))
+        assert O.get_legal_moves(me, opp) == u(val)
+
+
+def test_legal_actions_match_children(bb):
+    player, p1, p2, legal = bb["pos_player"], bb["pos_p1"], bb["pos_p2"], bb["pos_legal"]
+    by_parent = {}
+    for par, a in zip(bb["ch_parent"], bb["ch_action"]):
+        by_parent.setdefault(int(par), []).append(int(a))
+    for i in range(len(player)):
+        p = _pos(int(player[i]), u(p1[i]), u(p2[i]), u(legal[i]))
+        assert O.legal_actions(p) == by_parent.get(i, [])
+
+
+def test_features(golden_dir):
+    f = np.load(golden_dir / "features.npz")
+    offs, foffs = f["chain_offsets"], f["feat_offsets"]
+    for c in range(len(offs) - 1):
+        rows = range(offs[c], offs[c + 1])
+        chain = [_pos(int(f["player"][r]), u(f["p1"][r]), u(f["p2"][r]), u(f["legal"][r])) for r in rows]
+        h, t = int(f["history_size"][c]), int(f["transform"][c])
+        got = O.features(chain[::-1], h, t).reshape(-1)
+        exp = f["features"][foffs[c]:foffs[c + 1]].astype(np.float32)
+        np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("case", json.load(open(__import__("pathlib").Path(__file__).parent
+                                               / "golden" / "mcts_known_answers.json"))["cases"],
+                         ids=lambda c: c["name"])
+def test_mcts_known_answers(case):
+    m = O.OracleMCTS(history_size=case["history_size"], num_simulations=case["num_simulations"],
+                     num_threads=case["num_threads"], batch_size=case["batch_size"],
+                     dirichlet_epsilon=case["dirichlet_epsilon"])
+    for a in case["actions"]:
+        m.apply_action(a)
+    stub = O.equivariant_stub if case["stub"] == "equivariant" else O.uniform_stub
+    m.search(stub)
+    assert m.visit_counts() == case["visit_counts"]
+
+
+def test_mcts_invariants_multi_thread_and_noise():
+    """Net effect of one simulation is N+1, W+v on the path;
+    visit sum over root children = sims minus root-batch-quirk selections."""
+    m = O.OracleMCTS(history_size=8, num_simulations=800, num_threads=2, batch_size=16,
+                     dirichlet_epsilon=0.25, game_key=7)
+    n = m.search(O.equivariant_stub)
+    assert n == 800
+    vc = m.visit_counts()
+    assert sum(vc) == 800 - 32  # first step: all 32 leaves stop at the unexpanded root
+    assert m.root_visit_count() == 800
+    q = m.mean_action_values()
+    assert all(-1.0 <= x <= 1.0 for x in q)
+    # tree reuse: visits persist in the chosen subtree
+    best = int(np.argmax(vc))
+    a = O.legal_actions(m.position())[best]
+    m.apply_action(a)
+    before = m.root_visit_count()
+    m.search(O.equivariant_stub)
+    assert m.root_visit_count() == before + 800
+
+
+def test_gamma_sampler_moments():
+    # Gamma(alpha,1) has mean alpha and variance alpha
+    for alpha in (0.3, 0.5, 1.0, 2.5):
+        xs = np.array([O.lib().orc_gamma(O.lib().orc_stream_key(99, e, 0), alpha) for e in range(20000)])
+        assert abs(xs.mean() - alpha) < 0.05 * max(alpha, 1.0)
+        assert abs(xs.var() - alpha) < 0.12 * max(alpha, 1.0)
+
+
+def test_portable_math_close_to_libm():
+    xs = np.linspace(1e-6, 20, 5000, dtype=np.float32)
+    lg = np.array([O.lib().orc_logf(float(x)) for x in xs])
+    assert np.max(np.abs(lg - np.log(xs.astype(np.float64)))) < 2e-6 * 20
+    es = np.linspace(-80, 10, 5000, dtype=np.float32)
+    ex = np.array([O.lib().orc_expf(float(x)) for x in es])
+    np.testing.assert_allclose(ex, np.exp(es.astype(np.float64)), rtol=3e-6)
+
+
+@pytest.mark.parametrize("name", ["tiny", "c128b9_h8", "c128b9_h4", "c256b19_h8"])
+def test_resnet_restatement_matches_reference(golden_dir, name):
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    meta = json.loads((golden_dir / "resnet_meta.json").read_text())[name]
+    g = np.load(golden_dir / "resnet.npz")
+    sd = alphazero_state_dict(meta["seed"], 1 + 2 * meta["history_size"], meta["conv_channels"],
+                              meta["num_residual_blocks"], meta["value_head_hidden_channels"])
+    wsum = float(sum(np.asarray(v, np.float64).sum() for v in sd.values()))
+    assert wsum == pytest.approx(meta["weight_sum"], rel=1e-12)
+    out = resnet_ref.forward(sd, torch.from_numpy(g[f"{name}_x"].astype(np.float32)))
+    np.testing.assert_allclose(out["policy"].numpy(), g[f"{name}_policy"], atol=2e-6, rtol=1e-4)
+    np.testing.assert_allclose(out["value"].numpy(), g[f"{name}_value"], atol=2e-6, rtol=1e-4)
