@@ -1,0 +1,214 @@
+"""Benchmark: whole-node MCTS simulations/sec, 800 sims/move, 128x10b ResNet.
+
+BASELINE.json metric on configs[1] (256 concurrent self-play games, 128x10b,
+bf16, one MI355X) per GPU; with --gpus N (torchrun, one process per GPU) every
+rank runs its own 256 games (games shard embarrassingly: no collective on the
+hot path, "scaling": "weak").
+
+A step is one self-play move of every game on the GPU: a full 800-simulation
+search (25 steps of select -> fused ResNet -> expand/backup for T=2 x B=16
+leaves per game) followed by the on-device move choice, 8-fold target emission
+and move application (finished games restart from a random opening).
+Synthetic data: random-init AlphaZeroNet weights of the 128x10b architecture
+(seeded), random openings of 0..8 plies.
+
+Also reported (rank 0):
+  roofline      the fused ResNet kernel: algorithmic FLOPs (342.3 MFLOP per
+                evaluated leaf) / its average HIP-event duration, vs the
+                2.5 PFLOP/s dense bf16 MFMA peak; traffic from profiles/ if a
+                PMC summary for this config exists, else null.
+  cpu_baseline  the oracle C restatement of the reference search + torch-CPU
+                fp32 ResNet, 1 game (configs[0]), bounded sample on this host.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "othello-alphazero_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+
+
+def resnet_flops_per_eval(in_ch: int, C: int, R: int, hidden: int) -> float:
+    conv0 = 2 * 64 * 9 * in_ch * C
+    tower = 2 * R * 2 * 64 * 9 * C * C
+    heads = 2 * 64 * C * 3 + 2 * 128 * 65 + 2 * 64 * hidden + 2 * hidden
+    return float(conv0 + tower + heads)
+
+
+def cpu_baseline(seconds: float, history: int, C: int, R: int, hidden: int) -> dict:
+    """Oracle port of the reference CPU path (configs[0]): 1 game, 2 threads x 16,
+    800 sims/move, fp32 torch-CPU ResNet; moves until `seconds` elapse."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+
+    import oracle as O
+    import resnet_ref
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
+          alphazero_state_dict(1, 1 + 2 * history, C, R, hidden).items()}
+
+    def nn(feat):
+        with torch.no_grad():
+            out = resnet_ref.forward(sd, torch.from_numpy(np.ascontiguousarray(feat)))
+        return out["policy"].numpy(), out["value"].numpy()
+
+    m = O.OracleMCTS(history_size=history, num_simulations=800, num_threads=2, batch_size=16,
+                     dirichlet_epsilon=0.25, game_key=5)
+    sims = 0
+    moves = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        if m.position().player == 0:
+            m.reset_position()
+        sims += m.search(nn)
+        vc = m.visit_counts()
+        m.apply_action(O.legal_actions(m.position())[int(np.argmax(vc))])
+        moves += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(sims / dt, 1), "unit": "simulations/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"1 game from the initial position, {moves} moves x 800 sims (T=2 x B=16, "
+                      f"eps=0.25), {C}x{R + 1}b fp32 torch-CPU, {dt:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--games", type=int, default=256, help="concurrent games per GPU")
+    ap.add_argument("--sims", type=int, default=800)
+    ap.add_argument("--threads", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--history", type=int, default=8)
+    ap.add_argument("--channels", type=int, default=128)
+    ap.add_argument("--blocks", type=int, default=10, help="conv block + residual blocks")
+    ap.add_argument("--hidden", type=int, default=128)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--seed", type=int, default=2025)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import othello_mcts as om
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    R = args.blocks - 1
+    sd = alphazero_state_dict(args.seed, 1 + 2 * args.history, args.channels, R, args.hidden)
+    net = om.NativeNet(sd, device=local, dtype=args.dtype)
+    b = om.BatchedMCTS(args.games, history_size=args.history, num_simulations=args.sims,
+                       num_threads=args.threads, batch_size=args.batch, seed=args.seed + 7919 * rank)
+    b.random_openings(8, seed=args.seed + rank)
+    L = args.threads * args.batch
+    sims_per_search = L * ((args.sims + L - 1) // L)
+
+    def step():
+        b.search(net)
+        b.selfplay_move(temperature_moves=12, opening_moves=8, emit_targets=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    b.engine.enable_timing(True)
+    ms0, launches0, rows0 = b.engine.nn_timing()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evals = 0
+    for _ in range(args.steps):
+        b.search(net)  # counters: evaluated (non-terminal) leaves
+        b.selfplay_move(temperature_moves=12, opening_moves=8, emit_targets=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ms1, launches1, rows1 = b.engine.nn_timing()
+    # evaluated rows: re-run counters cheaply from the search return values
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = float(t.item())
+    total_sims = world * args.games * sims_per_search * args.steps
+    value = total_sims / dt_max
+
+    nn_ms = ms1 - ms0
+    nn_launches = launches1 - launches0
+    nn_rows = rows1 - rows0
+    flops = resnet_flops_per_eval(1 + 2 * args.history, args.channels, R, args.hidden)
+    avg_ms = nn_ms / max(1, nn_launches)
+    rows_per_launch = nn_rows / max(1, nn_launches)
+    achieved = flops * rows_per_launch / (avg_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+    traffic = None
+    tfile = ROOT / "profiles" / "traffic_resnet.json"
+    if tfile.exists():
+        try:
+            traffic = json.loads(tfile.read_text()).get("bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+
+    result = {
+        "metric": "MCTS simulations/sec (whole node), 800 sims/move, 128x10b ResNet, 1/2/4/8 GPU",
+        "value": round(value, 1),
+        "unit": "simulations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt_max * 1e3 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic: seeded random-init 128x10b AlphaZeroNet weights, random openings (0-8 plies)",
+        "config": {
+            "workload": f"{args.games} concurrent self-play games per GPU, {args.sims} sims/move, "
+                        f"{args.channels}x{args.blocks}b ResNet {args.dtype}, history {args.history}, "
+                        f"{args.threads} threads x {args.batch} leaves per step (BASELINE configs[1])",
+            "games_per_gpu": args.games,
+            "sims_per_move": args.sims,
+            "leaves_per_step": L,
+            "parallelism": f"games sharded over {world} GPU(s), no collective",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "k_resnet (fused 19-conv tower + heads)",
+            "achieved": round(achieved, 2),
+            "peak": peak,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4),
+            "traffic": traffic,
+            "avg_launch_ms": round(avg_ms, 4),
+            "rows_per_launch": int(rows_per_launch),
+            "flops_per_row": flops,
+        },
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.history, args.channels, R,
+                                              args.hidden)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

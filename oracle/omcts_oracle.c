@@ -105,6 +105,29 @@ int orc_legal_actions(const orc_pos *p, int32_t *actions_out) {
     return n;
 }
 
+void orc_legal_moves_n(const uint64_t *me, const uint64_t *opp, uint64_t *out, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) out[i] = orc_get_legal_moves(me[i], opp[i]);
+}
+
+void orc_flips_n(const uint64_t *mv, const uint64_t *me, const uint64_t *opp, uint64_t *out, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) out[i] = orc_get_flips(mv[i], me[i], opp[i]);
+}
+
+void orc_apply_action_n(const int32_t *player, const uint64_t *p1, const uint64_t *p2,
+                        const uint64_t *legal, const uint64_t *next_legal, const int32_t *action,
+                        int32_t *o_player, uint64_t *o_p1, uint64_t *o_p2, uint64_t *o_legal,
+                        uint64_t *o_next, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) {
+        orc_pos p = {player[i], p1[i], p2[i], legal[i], next_legal[i]}, c;
+        orc_apply_action(&p, action[i], &c);
+        o_player[i] = c.player;
+        o_p1[i] = c.p1;
+        o_p2[i] = c.p2;
+        o_legal[i] = c.legal;
+        o_next[i] = c.next_legal;
+    }
+}
+
 /* transformation.h:40-57: optional horizontal flip (t odd), then t/2
  * clockwise rotations (row,col) -> (col, 7-row); pass is fixed. */
 int orc_transform_action(int action, int t) {

@@ -47,6 +47,14 @@ void orc_apply_action(const orc_pos *p, int action, orc_pos *out);
 /* ascending square order, {64} when the side to move must pass, {} if terminal */
 int orc_legal_actions(const orc_pos *p, int32_t *actions_out);
 int orc_transform_action(int action, int t);
+/* batched loops (n elements) for large-size parity checks */
+void orc_legal_moves_n(const uint64_t *me, const uint64_t *opp, uint64_t *out, int64_t n);
+void orc_flips_n(const uint64_t *mv, const uint64_t *me, const uint64_t *opp, uint64_t *out, int64_t n);
+/* positions as 5 arrays: player (i32), p1, p2, legal, next_legal */
+void orc_apply_action_n(const int32_t *player, const uint64_t *p1, const uint64_t *p2,
+                        const uint64_t *legal, const uint64_t *next_legal, const int32_t *action,
+                        int32_t *o_player, uint64_t *o_p1, uint64_t *o_p2, uint64_t *o_legal,
+                        uint64_t *o_next, int64_t n);
 /* features of a chain: chain[0] = current position, chain[1] its parent, ...
  * (n_chain entries); writes (1 + 2*history_size) * 64 floats */
 void orc_features(const orc_pos *chain, int n_chain, int history_size, int t, float *out);

@@ -67,6 +67,9 @@ def lib():
             "orc_apply_action": (None, [P(CPos), i32, P(CPos)]),
             "orc_legal_actions": (i32, [P(CPos), P(ctypes.c_int32)]),
             "orc_transform_action": (i32, [i32, i32]),
+            "orc_legal_moves_n": (None, [vp, vp, vp, ctypes.c_int64]),
+            "orc_flips_n": (None, [vp, vp, vp, vp, ctypes.c_int64]),
+            "orc_apply_action_n": (None, [vp] * 11 + [ctypes.c_int64]),
             "orc_features": (None, [P(CPos), i32, i32, i32, P(f32)]),
             "orc_mix64": (u64, [u64]),
             "orc_stream_key": (u64, [u64, u64, ctypes.c_uint32]),
@@ -122,6 +125,36 @@ def legal_actions(p: CPos) -> list[int]:
     buf = (ctypes.c_int32 * 65)()
     n = lib().orc_legal_actions(ctypes.byref(p), buf)
     return list(buf[:n])
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def legal_moves_n(me: np.ndarray, opp: np.ndarray) -> np.ndarray:
+    me = np.ascontiguousarray(me, np.uint64)
+    opp = np.ascontiguousarray(opp, np.uint64)
+    out = np.empty_like(me)
+    lib().orc_legal_moves_n(_p(me), _p(opp), _p(out), me.size)
+    return out
+
+
+def flips_n(mv: np.ndarray, me: np.ndarray, opp: np.ndarray) -> np.ndarray:
+    mv, me, opp = (np.ascontiguousarray(x, np.uint64) for x in (mv, me, opp))
+    out = np.empty_like(me)
+    lib().orc_flips_n(_p(mv), _p(me), _p(opp), _p(out), me.size)
+    return out
+
+
+def apply_action_n(player, p1, p2, legal, next_legal, action):
+    player = np.ascontiguousarray(player, np.int32)
+    p1, p2, legal, next_legal = (np.ascontiguousarray(x, np.uint64) for x in (p1, p2, legal, next_legal))
+    action = np.ascontiguousarray(action, np.int32)
+    n = player.size
+    out = [np.empty(n, np.int32)] + [np.empty(n, np.uint64) for _ in range(4)]
+    lib().orc_apply_action_n(_p(player), _p(p1), _p(p2), _p(legal), _p(next_legal), _p(action),
+                             *(_p(x) for x in out), n)
+    return out
 
 
 def transform_action(a: int, t: int) -> int:

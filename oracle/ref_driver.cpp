@@ -146,12 +146,17 @@ void cmd_features(int n_games) {
 void cmd_strings(int n_games) {
     for (int g = 0; g < n_games; ++g) {
         othello::Position p = othello::Position::initial_position();
-        int plies = pick(61);
+        int plies = g == 0 ? 0 : pick(61);
+        std::vector<int> seq;
         for (int k = 0; k < plies && !p.is_terminal(); ++k) {
             std::vector<int> actions = p.legal_actions();
-            p = p.apply_action(actions[pick(static_cast<int>(actions.size()))]);
+            seq.push_back(actions[pick(static_cast<int>(actions.size()))]);
+            p = p.apply_action(seq.back());
         }
         print_position("P", p);
+        std::printf("Q");
+        for (int a : seq) std::printf(" %d", a);
+        std::printf("\n");
         std::string s = p.to_string();
         std::printf("S");
         for (unsigned char ch : s) std::printf(" %02x", ch);

@@ -1,0 +1,89 @@
+"""Build the MI355X-native othello_mcts extension in-tree.
+
+  liboamd.so               HIP kernels (tree.hip, resnet.hip) + the C ABI (capi.hip),
+                           hipcc --offload-arch=gfx950
+  _othello_mcts_impl*.so   pybind11 host layer (pybind_module.cpp) over the C ABI
+
+Both land in othello-alphazero_amd/othello_mcts/ (git-ignored, shipped to the
+GPU box with the snapshot). Usage: python othello-alphazero_amd/build.py [-j N]
+"""
+
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+PKG = HERE / "othello_mcts"
+INCLUDE = HERE.parent / "include"
+BUILD = HERE / "build"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("OAMD_ARCH", "gfx950")
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", str(CSRC), "-I", str(INCLUDE),
+          "-Wall", "-Wno-unused-function", "-fno-gpu-rdc"]
+# tree.hip / rng.h / capi.hip tables must reproduce the reference's float
+# arithmetic bit for bit: no FMA contraction, IEEE division and sqrt.
+EXACT = ["-ffp-contract=off", "-fno-fast-math"]
+UNITS = {
+    "tree.hip": EXACT,
+    "capi.hip": EXACT,
+    "resnet.hip": [],
+}
+
+
+def run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise SystemExit(f"build failed: {cmd[-1]}")
+    if r.stderr.strip():
+        sys.stderr.write(r.stderr)
+
+
+def newer(out: Path, deps: list[Path]) -> bool:
+    return out.exists() and all(out.stat().st_mtime >= d.stat().st_mtime for d in deps)
+
+
+def build(jobs: int = 4, force: bool = False) -> None:
+    BUILD.mkdir(exist_ok=True)
+    headers = list(CSRC.glob("*.h")) + [INCLUDE / "othello_mcts_amd.h"]
+    objs = []
+    todo = []
+    for unit, extra in UNITS.items():
+        src = CSRC / unit
+        obj = BUILD / (unit + ".o")
+        objs.append(obj)
+        if force or not newer(obj, [src, *headers, Path(__file__)]):
+            todo.append([HIPCC, *COMMON, *extra, "-c", str(src), "-o", str(obj)])
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(run, todo))
+    lib = PKG / "liboamd.so"
+    if force or todo or not lib.exists():
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs)])
+
+    # pybind11 host layer: plain C++ against the C ABI, no torch headers
+    import pybind11
+
+    ext = sysconfig.get_config_var("EXT_SUFFIX")
+    mod = PKG / f"_othello_mcts_impl{ext}"
+    src = CSRC / "pybind_module.cpp"
+    if force or not newer(mod, [src, INCLUDE / "othello_mcts_amd.h", lib, Path(__file__)]):
+        run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
+             "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], "-I", str(INCLUDE),
+             str(src), "-o", str(mod), "-L", str(PKG), "-loamd", "-Wl,-rpath,$ORIGIN"])
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", "--jobs", type=int, default=4)
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    build(a.jobs, a.force)
+    print("built", *sorted(p.name for p in PKG.glob("*.so")))

@@ -1,0 +1,850 @@
+// C ABI (include/othello_mcts_amd.h): engine / net lifetime, validation with
+// the reference's exception messages, host-side weight folding and packing,
+// and the search step sequence. All compute is in tree.hip / resnet.hip.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/othello_mcts_amd.h"
+#include "bitboard.h"
+#include "engine.h"
+#include "kernels.h"
+
+using namespace oamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+    do {                                                                              \
+        hipError_t _e = (expr);                                                       \
+        if (_e != hipSuccess)                                                         \
+            return fail(OAMD_RUNTIME, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define LAUNCHCHK()                                                                       \
+    do {                                                                                  \
+        hipError_t _e = hipGetLastError();                                                \
+        if (_e != hipSuccess) return fail(OAMD_RUNTIME, std::string("kernel launch: ") + hipGetErrorString(_e)); \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+int dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) return OAMD_OK;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T));
+    if (e != hipSuccess) return fail(OAMD_RUNTIME, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return OAMD_OK;
+}
+
+template <typename T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+std::string fstr(float v) { return std::to_string(v); }
+
+// mcts.cpp:167-241 (messages verbatim) + the native engine's own limits
+int validate_config(const oamd_search_config* c) {
+    if (c->history_size < 1)
+        return fail(OAMD_INVALID_ARGUMENT,
+                    "Expected history_size >= 1, but got " + std::to_string(c->history_size) + ".");
+    if (c->history_size > kMaxHistory)
+        return fail(OAMD_INVALID_ARGUMENT, "Expected history_size <= 15 (native engine limit), but got " +
+                                               std::to_string(c->history_size) + ".");
+    if (c->num_simulations < 1)
+        return fail(OAMD_INVALID_ARGUMENT, "Expected num_simulations >= 1, but got " +
+                                               std::to_string(c->num_simulations) + ".");
+    if (c->num_threads < 1)
+        return fail(OAMD_INVALID_ARGUMENT,
+                    "Expected num_threads >= 1, but got " + std::to_string(c->num_threads) + ".");
+    if (c->batch_size < 1)
+        return fail(OAMD_INVALID_ARGUMENT,
+                    "Expected batch_size >= 1, but got " + std::to_string(c->batch_size) + ".");
+    if ((int64_t)c->num_threads * c->batch_size > kMaxLeaves)
+        return fail(OAMD_INVALID_ARGUMENT,
+                    "Expected num_threads * batch_size <= 1024 (native engine limit), but got " +
+                        std::to_string((int64_t)c->num_threads * c->batch_size) + ".");
+    if (!(c->c_puct_base > 0.0f))
+        return fail(OAMD_INVALID_ARGUMENT, "Expected c_puct_base > 0.0, but got " + fstr(c->c_puct_base) + ".");
+    if (!(c->c_puct_init >= 0.0f))
+        return fail(OAMD_INVALID_ARGUMENT, "Expected c_puct_init >= 0.0, but got " + fstr(c->c_puct_init) + ".");
+    if (!(0.0f <= c->dirichlet_epsilon && c->dirichlet_epsilon <= 1.0f))
+        return fail(OAMD_INVALID_ARGUMENT, "Expected 0.0 <= dirichlet_epsilon <= 1.0, but got " +
+                                               fstr(c->dirichlet_epsilon) + ".");
+    if (!(c->dirichlet_alpha >= 0.0f))
+        return fail(OAMD_INVALID_ARGUMENT,
+                    "Expected dirichlet_alpha >= 0.0, but got " + fstr(c->dirichlet_alpha) + ".");
+    return OAMD_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// engine
+// ===========================================================================
+struct oamd_engine {
+    int device = 0;
+    int G = 0;
+    int64_t cap = 0;
+    oamd_search_config cfg{};
+    hipStream_t stream = nullptr;
+    uint64_t seed = 0;
+
+    NodeLink* link = nullptr;
+    NodeStat* stat = nullptr;
+    NodePos* pos = nullptr;
+    GameState* games = nullptr;
+    // per-row buffers (sized for rows_cap rows)
+    int64_t rows_cap = 0;
+    int fw_cap = 0;
+    int32_t* leaf = nullptr;
+    int32_t* depth = nullptr;
+    int32_t* trans = nullptr;
+    int32_t* path = nullptr;
+    uint64_t* feat = nullptr;
+    float* policy = nullptr;
+    float* value = nullptr;
+    uint8_t* flags = nullptr;
+    float* explore_tab = nullptr;
+    float* sqrt_tab = nullptr;
+    unsigned long long* counters = nullptr;
+    // query scratch
+    oamd_root_info* info_dev = nullptr;
+    int32_t* visits_dev = nullptr;
+    float* q_dev = nullptr;
+    float* spd_dev = nullptr;  // self-play data scratch (8*(1+2H)*64 + 8*65)
+    // search state
+    int steps_left = 0;
+    int step_phase = 0;  // 0 = expect select, 1 = expect backup
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;
+    float nn_ms = 0.0f;
+    int64_t nn_launches = 0;
+    int64_t nn_rows = 0;
+
+    int L() const { return cfg.num_threads * cfg.batch_size; }
+    int FW() const { return feature_words(cfg.history_size); }
+
+    EngineView view() const {
+        EngineView E;
+        E.G = G;
+        E.L = L();
+        E.H = cfg.history_size;
+        E.FW = FW();
+        E.cap = cap;
+        E.link = link;
+        E.stat = stat;
+        E.pos = pos;
+        E.games = games;
+        E.leaf = leaf;
+        E.depth = depth;
+        E.trans = trans;
+        E.path = path;
+        E.feat = feat;
+        E.policy = policy;
+        E.value = value;
+        E.explore_tab = explore_tab;
+        E.sqrt_tab = sqrt_tab;
+        E.c_base = cfg.c_puct_base;
+        E.c_init = cfg.c_puct_init;
+        E.eps = cfg.dirichlet_epsilon;
+        E.alpha = cfg.dirichlet_alpha;
+        E.counters = counters;
+        return E;
+    }
+
+    int alloc_rows() {
+        const int64_t rows = (int64_t)G * L();
+        const int fw = FW();
+        if (rows <= rows_cap && fw <= fw_cap) return OAMD_OK;
+        dfree(leaf);
+        dfree(depth);
+        dfree(trans);
+        dfree(path);
+        dfree(feat);
+        dfree(policy);
+        dfree(value);
+        dfree(flags);
+        int rc;
+        if ((rc = dalloc(&leaf, rows)) || (rc = dalloc(&depth, rows)) || (rc = dalloc(&trans, rows)) ||
+            (rc = dalloc(&path, rows * kMaxDepth)) || (rc = dalloc(&feat, rows * fw)) ||
+            (rc = dalloc(&policy, rows * 65)) || (rc = dalloc(&value, rows)) || (rc = dalloc(&flags, rows)))
+            return rc;
+        HIPCHK(hipMemset(policy, 0, rows * 65 * sizeof(float)));
+        HIPCHK(hipMemset(value, 0, rows * sizeof(float)));
+        rows_cap = rows;
+        fw_cap = fw;
+        return OAMD_OK;
+    }
+
+    // exploration_rate table with the HOST's logf (bit-identical to the
+    // reference's std::log(float), search_thread.cpp:198-203)
+    int build_tables() {
+        std::vector<float> ex(kExploreTab), sq(kExploreTab);
+        for (int n = 0; n < kExploreTab; ++n) {
+            ex[n] = std::log(((float)(1 + n) + cfg.c_puct_base) / cfg.c_puct_base) + cfg.c_puct_init;
+            sq[n] = std::sqrt((float)n);
+        }
+        HIPCHK(hipMemcpy(explore_tab, ex.data(), ex.size() * sizeof(float), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(sqrt_tab, sq.data(), sq.size() * sizeof(float), hipMemcpyHostToDevice));
+        return OAMD_OK;
+    }
+
+    ~oamd_engine() {
+        DeviceGuard dg(device);
+        dfree(link);
+        dfree(stat);
+        dfree(pos);
+        dfree(games);
+        dfree(leaf);
+        dfree(depth);
+        dfree(trans);
+        dfree(path);
+        dfree(feat);
+        dfree(policy);
+        dfree(value);
+        dfree(flags);
+        dfree(explore_tab);
+        dfree(sqrt_tab);
+        dfree(counters);
+        dfree(info_dev);
+        dfree(visits_dev);
+        dfree(q_dev);
+        dfree(spd_dev);
+        for (auto e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+// ===========================================================================
+// net
+// ===========================================================================
+struct oamd_net {
+    int device = 0;
+    oamd_net_desc desc{};
+    uint16_t* w = nullptr;
+    float* bias = nullptr;
+    float* head = nullptr;
+    bool loaded = false;
+    std::vector<std::string> keys;
+    std::vector<int64_t> numel;
+
+    NetView view() const {
+        NetView N;
+        N.cin = desc.in_channels;
+        N.C = desc.conv_channels;
+        N.R = desc.num_residual_blocks;
+        N.hidden = desc.value_head_hidden_channels;
+        N.dtype = desc.dtype;
+        N.w = w;
+        N.bias = bias;
+        N.head = head;
+        return N;
+    }
+    ~oamd_net() {
+        DeviceGuard dg(device);
+        dfree(w);
+        dfree(bias);
+        dfree(head);
+    }
+};
+
+extern "C" {
+
+const char* oamd_last_error(void) { return g_err.c_str(); }
+int oamd_abi_version(void) { return OAMD_ABI_VERSION; }
+
+int oamd_device_count(int32_t* out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return OAMD_OK;
+}
+
+// ---------------------------------------------------------------- bitboards
+int oamd_get_legal_moves(const uint64_t* me, const uint64_t* opp, uint64_t* out, int64_t n, void* stream) {
+    if (n < 0) return fail(OAMD_INVALID_ARGUMENT, "n must be >= 0");
+    launch_legal_moves(me, opp, out, n, (hipStream_t)stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_get_flips(const uint64_t* mv, const uint64_t* me, const uint64_t* opp, uint64_t* out, int64_t n,
+                   void* stream) {
+    if (n < 0) return fail(OAMD_INVALID_ARGUMENT, "n must be >= 0");
+    launch_flips(mv, me, opp, out, n, (hipStream_t)stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_apply_action(const oamd_position* in, const int32_t* actions, oamd_position* out, int64_t n,
+                      void* stream) {
+    static_assert(sizeof(oamd_position) == sizeof(Pos), "layout");
+    if (n < 0) return fail(OAMD_INVALID_ARGUMENT, "n must be >= 0");
+    launch_apply_positions(reinterpret_cast<const Pos*>(in), actions, reinterpret_cast<Pos*>(out), n,
+                           (hipStream_t)stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_initial_position(oamd_position* out) {
+    const Pos p = initial_position();
+    std::memcpy(out, &p, sizeof(Pos));
+    return OAMD_OK;
+}
+
+uint64_t oamd_host_legal_moves(uint64_t me, uint64_t opp) { return legal_moves(me, opp); }
+uint64_t oamd_host_flips(uint64_t mv, uint64_t me, uint64_t opp) { return flips(mv, me, opp); }
+void oamd_host_apply_action(const oamd_position* in, int32_t action, oamd_position* out) {
+    Pos p;
+    std::memcpy(&p, in, sizeof(Pos));
+    const Pos c = apply_action(p, action);
+    std::memcpy(out, &c, sizeof(Pos));
+}
+
+// ---------------------------------------------------------------- net
+int oamd_net_create(int32_t device, const oamd_net_desc* d, oamd_net** out) {
+    *out = nullptr;
+    if (d->in_channels < 1 || d->in_channels > 31)
+        return fail(OAMD_INVALID_ARGUMENT, "in_channels must be in [1, 31], got " + std::to_string(d->in_channels));
+    if (d->conv_channels != 128 && d->conv_channels != 256)
+        return fail(OAMD_INVALID_ARGUMENT,
+                    "conv_channels must be 128 or 256 for the native net, got " + std::to_string(d->conv_channels));
+    if (d->num_residual_blocks < 0)
+        return fail(OAMD_INVALID_ARGUMENT, "num_residual_blocks must be >= 0");
+    if (d->value_head_hidden_channels < 1)
+        return fail(OAMD_INVALID_ARGUMENT, "value_head_hidden_channels must be >= 1");
+    if (d->num_squares != 64 || d->num_actions != 65)
+        return fail(OAMD_INVALID_ARGUMENT, "num_squares must be 64 and num_actions 65");
+    if (d->dtype != OAMD_BF16 && d->dtype != OAMD_FP16)
+        return fail(OAMD_INVALID_ARGUMENT, "dtype must be OAMD_BF16 or OAMD_FP16");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(OAMD_RUNTIME, "no HIP device available");
+    if (device < 0 || device >= n) return fail(OAMD_INVALID_ARGUMENT, "bad device ordinal");
+    DeviceGuard dg(device);
+    auto* net = new oamd_net();
+    net->device = device;
+    net->desc = *d;
+    const int C = d->conv_channels, R = d->num_residual_blocks, hid = d->value_head_hidden_channels;
+    int rc;
+    if ((rc = dalloc(&net->w, resnet_packed_weight_elems(C, R))) ||
+        (rc = dalloc(&net->bias, (size_t)(1 + 2 * R) * C)) ||
+        (rc = dalloc(&net->head, resnet_head_floats(C, hid)))) {
+        delete net;
+        return rc;
+    }
+    // state_dict keys (neural_net.py:9-172), num_batches_tracked omitted
+    auto conv = [&](const std::string& p, int64_t cout, int64_t cin, int64_t k) {
+        net->keys.push_back(p + ".weight");
+        net->numel.push_back(cout * cin * k * k);
+        net->keys.push_back(p + ".bias");
+        net->numel.push_back(cout);
+    };
+    auto bn = [&](const std::string& p, int64_t c) {
+        for (const char* s : {".weight", ".bias", ".running_mean", ".running_var"}) {
+            net->keys.push_back(p + s);
+            net->numel.push_back(c);
+        }
+    };
+    auto lin = [&](const std::string& p, int64_t fin, int64_t fout) {
+        net->keys.push_back(p + ".weight");
+        net->numel.push_back(fin * fout);
+        net->keys.push_back(p + ".bias");
+        net->numel.push_back(fout);
+    };
+    conv("conv_block.conv", C, d->in_channels, 3);
+    bn("conv_block.norm", C);
+    for (int i = 0; i < R; ++i) {
+        const std::string p = "residual_blocks." + std::to_string(i);
+        conv(p + ".conv1", C, C, 3);
+        bn(p + ".norm1", C);
+        conv(p + ".conv2", C, C, 3);
+        bn(p + ".norm2", C);
+    }
+    conv("policy_head.conv", 2, C, 1);
+    bn("policy_head.norm", 2);
+    lin("policy_head.linear", 128, 65);
+    conv("value_head.conv", 1, C, 1);
+    bn("value_head.norm", 1);
+    lin("value_head.linear1", 64, hid);
+    lin("value_head.linear2", hid, 1);
+    *out = net;
+    return OAMD_OK;
+}
+
+int oamd_net_destroy(oamd_net* net) {
+    delete net;
+    return OAMD_OK;
+}
+
+int oamd_net_state_size(const oamd_net* net, int32_t* n) {
+    *n = (int32_t)net->keys.size();
+    return OAMD_OK;
+}
+
+int oamd_net_state_key(const oamd_net* net, int32_t i, const char** key, int64_t* numel) {
+    if (i < 0 || i >= (int32_t)net->keys.size()) return fail(OAMD_OUT_OF_RANGE, "state index out of range");
+    *key = net->keys[i].c_str();
+    *numel = net->numel[i];
+    return OAMD_OK;
+}
+
+static uint16_t f32_to_bf16_rne(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+static uint16_t f32_to_f16(float f) {
+    _Float16 h = (_Float16)f;
+    uint16_t u;
+    std::memcpy(&u, &h, 2);
+    return u;
+}
+
+int oamd_net_load_state(oamd_net* net, const float* const* t, int32_t n_tensors) {
+    if (n_tensors != (int32_t)net->keys.size())
+        return fail(OAMD_INVALID_ARGUMENT, "expected " + std::to_string(net->keys.size()) + " tensors, got " +
+                                               std::to_string(n_tensors));
+    const auto& d = net->desc;
+    const int C = d.conv_channels, R = d.num_residual_blocks, hid = d.value_head_hidden_channels;
+    const double eps = 1e-5;  // torch.nn.BatchNorm2d default
+    int ti = 0;
+    std::vector<uint16_t> packed(resnet_packed_weight_elems(C, R));
+    std::vector<float> bias((size_t)(1 + 2 * R) * C);
+    size_t ks_global = 0;
+    // fold BN into a 3x3 conv and pack in MFMA B-fragment order:
+    // [ks = tap*CB + cb][ntile][lane][8], k_local = 8*(lane>>4)+j, n = ntile*16 + (lane&15)
+    auto pack_conv = [&](int layer, int cin, int cin_pad) {
+        const float* W = t[ti++];
+        const float* b = t[ti++];
+        const float* g = t[ti++];
+        const float* be = t[ti++];
+        const float* mu = t[ti++];
+        const float* var = t[ti++];
+        std::vector<double> scale(C);
+        for (int n = 0; n < C; ++n) {
+            scale[n] = (double)g[n] / std::sqrt((double)var[n] + eps);
+            bias[(size_t)layer * C + n] = (float)(((double)b[n] - (double)mu[n]) * scale[n] + (double)be[n]);
+        }
+        const int CB = cin_pad / 32;
+        for (int tap = 0; tap < 9; ++tap) {
+            for (int cb = 0; cb < CB; ++cb) {
+                const size_t ks = ks_global + (size_t)tap * CB + cb;
+                for (int nt = 0; nt < C / 16; ++nt)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int j = 0; j < 8; ++j) {
+                            const int ci = cb * 32 + 8 * (lane >> 4) + j;
+                            const int n = nt * 16 + (lane & 15);
+                            double v = 0.0;
+                            if (ci < cin) v = (double)W[((size_t)n * cin + ci) * 9 + tap] * scale[n];
+                            const size_t idx = (((ks * (C / 16) + nt) * 64) + lane) * 8 + j;
+                            packed[idx] = d.dtype == OAMD_BF16 ? f32_to_bf16_rne((float)v) : f32_to_f16((float)v);
+                        }
+            }
+        }
+        ks_global += (size_t)9 * CB;
+    };
+    pack_conv(0, d.in_channels, 32);
+    for (int i = 0; i < R; ++i) {
+        pack_conv(1 + 2 * i, C, C);
+        pack_conv(2 + 2 * i, C, C);
+    }
+    // heads (fp32; 1x1 conv + BN folded)
+    std::vector<float> head(resnet_head_floats(C, hid));
+    const int HL_pcw = 0, HL_pcb = HL_pcw + 2 * C, HL_vcw = HL_pcb + 2, HL_vcb = HL_vcw + C,
+              HL_plw = HL_vcb + 1, HL_plb = HL_plw + 128 * 65, HL_v1w = HL_plb + 65, HL_v1b = HL_v1w + 64 * hid,
+              HL_v2w = HL_v1b + hid, HL_v2b = HL_v2w + hid;
+    {
+        const float* W = t[ti++];
+        const float* b = t[ti++];
+        const float* g = t[ti++];
+        const float* be = t[ti++];
+        const float* mu = t[ti++];
+        const float* var = t[ti++];
+        for (int c = 0; c < 2; ++c) {
+            const double s = (double)g[c] / std::sqrt((double)var[c] + eps);
+            for (int ch = 0; ch < C; ++ch) head[HL_pcw + c * C + ch] = (float)((double)W[c * C + ch] * s);
+            head[HL_pcb + c] = (float)(((double)b[c] - (double)mu[c]) * s + (double)be[c]);
+        }
+        const float* LW = t[ti++];
+        const float* LB = t[ti++];
+        for (int a = 0; a < 65; ++a) {
+            for (int i = 0; i < 128; ++i) head[HL_plw + i * 65 + a] = LW[a * 128 + i];
+            head[HL_plb + a] = LB[a];
+        }
+    }
+    {
+        const float* W = t[ti++];
+        const float* b = t[ti++];
+        const float* g = t[ti++];
+        const float* be = t[ti++];
+        const float* mu = t[ti++];
+        const float* var = t[ti++];
+        const double s = (double)g[0] / std::sqrt((double)var[0] + eps);
+        for (int ch = 0; ch < C; ++ch) head[HL_vcw + ch] = (float)((double)W[ch] * s);
+        head[HL_vcb] = (float)(((double)b[0] - (double)mu[0]) * s + (double)be[0]);
+        const float* W1 = t[ti++];
+        const float* B1 = t[ti++];
+        for (int j = 0; j < hid; ++j) {
+            for (int sq = 0; sq < 64; ++sq) head[HL_v1w + sq * hid + j] = W1[j * 64 + sq];
+            head[HL_v1b + j] = B1[j];
+        }
+        const float* W2 = t[ti++];
+        const float* B2 = t[ti++];
+        for (int j = 0; j < hid; ++j) head[HL_v2w + j] = W2[j];
+        head[HL_v2b] = B2[0];
+    }
+    DeviceGuard dg(net->device);
+    HIPCHK(hipMemcpy(net->w, packed.data(), packed.size() * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(net->bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(net->head, head.data(), head.size() * 4, hipMemcpyHostToDevice));
+    net->loaded = true;
+    return OAMD_OK;
+}
+
+int oamd_net_forward(oamd_net* net, const float* features, int32_t rows, float* policy, float* value,
+                     void* stream) {
+    if (!net->loaded) return fail(OAMD_INVALID_ARGUMENT, "net weights not loaded");
+    if (rows < 0) return fail(OAMD_INVALID_ARGUMENT, "rows must be >= 0");
+    DeviceGuard dg(net->device);
+    launch_resnet_f32(net->view(), features, rows, policy, value, (hipStream_t)stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+// ---------------------------------------------------------------- engine
+int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity, const oamd_search_config* cfg,
+                       uint64_t seed, oamd_engine** out) {
+    *out = nullptr;
+    int rc = validate_config(cfg);
+    if (rc) return rc;
+    if (num_games < 1) return fail(OAMD_INVALID_ARGUMENT, "num_games must be >= 1");
+    if (node_capacity == 0) node_capacity = (int64_t)1 << 20;
+    if (node_capacity < 128 || node_capacity > ((int64_t)1 << 30))
+        return fail(OAMD_INVALID_ARGUMENT, "node_capacity must be in [128, 2^30]");
+    if ((int64_t)num_games * node_capacity > ((int64_t)1 << 36))
+        return fail(OAMD_INVALID_ARGUMENT, "num_games * node_capacity too large");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(OAMD_RUNTIME, "no HIP device available");
+    if (device < 0 || device >= n) return fail(OAMD_INVALID_ARGUMENT, "bad device ordinal");
+    DeviceGuard dg(device);
+    auto* e = new oamd_engine();
+    e->device = device;
+    e->G = num_games;
+    e->cap = node_capacity;
+    e->cfg = *cfg;
+    e->seed = seed;
+    const size_t nodes = (size_t)num_games * node_capacity;
+    if ((rc = dalloc(&e->link, nodes)) || (rc = dalloc(&e->stat, nodes)) || (rc = dalloc(&e->pos, nodes)) ||
+        (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) ||
+        (rc = dalloc(&e->sqrt_tab, kExploreTab)) || (rc = dalloc(&e->counters, 2)) ||
+        (rc = dalloc(&e->info_dev, num_games)) || (rc = dalloc(&e->visits_dev, (size_t)num_games * 65)) ||
+        (rc = dalloc(&e->q_dev, (size_t)num_games * 65)) ||
+        (rc = dalloc(&e->spd_dev, (size_t)8 * (1 + 2 * kMaxHistory) * 64 + 8 * 65)) || (rc = e->alloc_rows()) ||
+        (rc = e->build_tables())) {
+        delete e;
+        return rc;
+    }
+    launch_reset(e->view(), -1, seed, nullptr);
+    hipError_t le = hipGetLastError();
+    if (le != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        delete e;
+        return fail(OAMD_RUNTIME, std::string("engine init: ") + hipGetErrorString(le));
+    }
+    *out = e;
+    return OAMD_OK;
+}
+
+int oamd_engine_destroy(oamd_engine* e) {
+    delete e;
+    return OAMD_OK;
+}
+
+int oamd_engine_set_config(oamd_engine* e, const oamd_search_config* cfg) {
+    int rc = validate_config(cfg);
+    if (rc) return rc;
+    DeviceGuard dg(e->device);
+    const bool tabs = cfg->c_puct_base != e->cfg.c_puct_base || cfg->c_puct_init != e->cfg.c_puct_init;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->cfg = *cfg;
+    if ((rc = e->alloc_rows())) return rc;
+    if (tabs && (rc = e->build_tables())) return rc;
+    e->step_phase = 0;
+    e->steps_left = 0;
+    return OAMD_OK;
+}
+
+int oamd_engine_get_config(const oamd_engine* e, oamd_search_config* cfg) {
+    *cfg = e->cfg;
+    return OAMD_OK;
+}
+
+int oamd_engine_num_games(const oamd_engine* e, int32_t* out) {
+    *out = e->G;
+    return OAMD_OK;
+}
+
+int oamd_engine_set_stream(oamd_engine* e, void* stream) {
+    e->stream = (hipStream_t)stream;
+    return OAMD_OK;
+}
+
+int oamd_engine_reset(oamd_engine* e, int32_t game, uint64_t seed) {
+    if (game < -1 || game >= e->G) return fail(OAMD_OUT_OF_RANGE, "game index out of range");
+    DeviceGuard dg(e->device);
+    launch_reset(e->view(), game, seed, e->stream);
+    LAUNCHCHK();
+    e->step_phase = 0;
+    e->steps_left = 0;
+    return OAMD_OK;
+}
+
+int oamd_engine_search_begin(oamd_engine* e, int32_t* steps) {
+    const int L = e->L();
+    e->steps_left = (e->cfg.num_simulations + L - 1) / L;  // search_thread.cpp:50-52
+    e->step_phase = 0;
+    if (steps) *steps = e->steps_left;
+    return OAMD_OK;
+}
+
+int oamd_engine_select(oamd_engine* e) {
+    if (e->steps_left <= 0 || e->step_phase != 0)
+        return fail(OAMD_INVALID_ARGUMENT, "select called out of order (search_begin / backup first)");
+    DeviceGuard dg(e->device);
+    launch_select(e->view(), e->stream);
+    LAUNCHCHK();
+    e->step_phase = 1;
+    return OAMD_OK;
+}
+
+int oamd_engine_leaf_flags(oamd_engine* e, uint8_t* host_out) {
+    DeviceGuard dg(e->device);
+    launch_leaf_flags(e->view(), e->flags, e->stream);
+    LAUNCHCHK();
+    HIPCHK(hipMemcpyAsync(host_out, e->flags, (size_t)e->G * e->L(), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return OAMD_OK;
+}
+
+int oamd_engine_features(oamd_engine* e, float* out, int32_t row_begin, int32_t rows) {
+    if (row_begin < 0 || rows < 0 || (int64_t)row_begin + rows > (int64_t)e->G * e->L())
+        return fail(OAMD_OUT_OF_RANGE, "row range out of range");
+    DeviceGuard dg(e->device);
+    launch_features_f32(e->view(), out, row_begin, rows, e->stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_engine_set_evaluation(oamd_engine* e, const float* pol, const float* val, int32_t row_begin,
+                               int32_t rows) {
+    if (row_begin < 0 || rows < 0 || (int64_t)row_begin + rows > (int64_t)e->G * e->L())
+        return fail(OAMD_OUT_OF_RANGE, "row range out of range");
+    DeviceGuard dg(e->device);
+    launch_set_evaluation(e->view(), pol, val, row_begin, rows, e->stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_engine_backup(oamd_engine* e) {
+    if (e->step_phase != 1) return fail(OAMD_INVALID_ARGUMENT, "backup called before select");
+    DeviceGuard dg(e->device);
+    launch_backup(e->view(), e->stream);
+    LAUNCHCHK();
+    e->step_phase = 0;
+    e->steps_left -= 1;
+    return OAMD_OK;
+}
+
+int oamd_engine_enable_timing(oamd_engine* e, int32_t enable) {
+    e->timing = enable != 0;
+    return OAMD_OK;
+}
+
+int oamd_engine_nn_timing(const oamd_engine* e, float* nn_ms, int64_t* launches, int64_t* rows) {
+    if (nn_ms) *nn_ms = e->nn_ms;
+    if (launches) *launches = e->nn_launches;
+    if (rows) *rows = e->nn_rows;
+    return OAMD_OK;
+}
+
+int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* evals) {
+    if (!net || !net->loaded) return fail(OAMD_INVALID_ARGUMENT, "native net not loaded");
+    if (net->device != e->device) return fail(OAMD_INVALID_ARGUMENT, "net and engine on different devices");
+    if (net->desc.in_channels != 1 + 2 * e->cfg.history_size)
+        return fail(OAMD_INVALID_ARGUMENT, "net in_channels != 1 + 2 * history_size");
+    DeviceGuard dg(e->device);
+    const int L = e->L();
+    const int steps = (e->cfg.num_simulations + L - 1) / L;
+    const EngineView E = e->view();
+    const NetView N = net->view();
+    const int rows = e->G * L;
+    if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
+    if (e->timing && (int)e->ev.size() < 2 * steps) {
+        while ((int)e->ev.size() < 2 * steps) {
+            hipEvent_t x;
+            HIPCHK(hipEventCreate(&x));
+            e->ev.push_back(x);
+        }
+    }
+    for (int s = 0; s < steps; ++s) {
+        launch_select(E, e->stream);
+        if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * s], e->stream));
+        launch_resnet_packed(N, E.feat, E.FW, E.H, rows, E.policy, E.value, e->stream);
+        if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * s + 1], e->stream));
+        launch_backup(E, e->stream);
+    }
+    LAUNCHCHK();
+    if (sims || evals || e->timing) {
+        unsigned long long c[2] = {0, 0};
+        if (sims || evals)
+            HIPCHK(hipMemcpyAsync(c, e->counters, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if (sims) *sims = (int64_t)c[0];
+        if (evals) *evals = (int64_t)c[1];
+        if (e->timing) {
+            for (int s = 0; s < steps; ++s) {
+                float ms = 0.0f;
+                HIPCHK(hipEventElapsedTime(&ms, e->ev[2 * s], e->ev[2 * s + 1]));
+                e->nn_ms += ms;
+            }
+            e->nn_launches += steps;
+            e->nn_rows += (int64_t)steps * rows;
+        }
+    }
+    e->step_phase = 0;
+    e->steps_left = 0;
+    return OAMD_OK;
+}
+
+int oamd_engine_root_info(oamd_engine* e, int32_t game, oamd_root_info* info, int32_t* visits, float* q) {
+    if (game < 0 || game >= e->G) return fail(OAMD_OUT_OF_RANGE, "game index out of range");
+    DeviceGuard dg(e->device);
+    launch_root_stats(e->view(), game, 1, e->info_dev, e->visits_dev, e->q_dev, 0, e->stream);
+    LAUNCHCHK();
+    oamd_root_info tmp;
+    HIPCHK(hipMemcpyAsync(&tmp, e->info_dev, sizeof(tmp), hipMemcpyDeviceToHost, e->stream));
+    int32_t v[65];
+    float qq[65];
+    HIPCHK(hipMemcpyAsync(v, e->visits_dev, sizeof(v), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(qq, e->q_dev, sizeof(qq), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (info) *info = tmp;
+    const int nc = tmp.num_children;
+    if (visits) std::memcpy(visits, v, sizeof(int32_t) * nc);
+    if (q) std::memcpy(q, qq, sizeof(float) * nc);
+    return OAMD_OK;
+}
+
+int oamd_engine_root_stats(oamd_engine* e, int32_t* visits_dev, float* q_dev, oamd_root_info* info_dev) {
+    DeviceGuard dg(e->device);
+    launch_root_stats(e->view(), 0, e->G, info_dev ? info_dev : e->info_dev, visits_dev ? visits_dev : e->visits_dev,
+                      q_dev ? q_dev : e->q_dev, 1, e->stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_engine_self_play_data(oamd_engine* e, int32_t game, float* features, float* policy) {
+    oamd_root_info info;
+    int rc = oamd_engine_root_info(e, game, &info, nullptr, nullptr);
+    if (rc) return rc;
+    if (info.position.player == 0)
+        return fail(OAMD_INVALID_ARGUMENT, "Self-play data cannot be generated from a terminal position.");
+    if (info.num_children == 0) return fail(OAMD_INVALID_ARGUMENT, "The root node has not been expanded yet.");
+    DeviceGuard dg(e->device);
+    const int C = 1 + 2 * e->cfg.history_size;
+    float* fd = e->spd_dev;
+    float* pd = e->spd_dev + (size_t)8 * C * 64;
+    launch_self_play_data(e->view(), game, fd, pd, e->stream);
+    LAUNCHCHK();
+    HIPCHK(hipMemcpyAsync(features, fd, sizeof(float) * 8 * C * 64, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(policy, pd, sizeof(float) * 8 * 65, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return OAMD_OK;
+}
+
+int oamd_engine_apply_action(oamd_engine* e, int32_t game, int32_t action) {
+    if (game < 0 || game >= e->G) return fail(OAMD_OUT_OF_RANGE, "game index out of range");
+    if (!(0 <= action && action < 65))
+        return fail(OAMD_OUT_OF_RANGE, "Expected 0 <= action < 65, but got " + std::to_string(action) + ".");
+    oamd_root_info info;
+    int rc = oamd_engine_root_info(e, game, &info, nullptr, nullptr);
+    if (rc) return rc;
+    if (action == 64) {
+        if (info.position.player == 0)
+            return fail(OAMD_INVALID_ARGUMENT, "Pass is not allowed in a terminal position.");
+        if (info.position.legal_moves != 0)
+            return fail(OAMD_INVALID_ARGUMENT, "Pass is not allowed when there are legal moves.");
+    } else if (((1ULL << (63 - action)) & info.position.legal_moves) == 0) {
+        return fail(OAMD_INVALID_ARGUMENT, std::to_string(action) + " is not a legal action.");
+    }
+    if (info.node_count + 1 > e->cap) return fail(OAMD_CAPACITY, "node pool exhausted");
+    DeviceGuard dg(e->device);
+    launch_apply_one(e->view(), game, action, e->stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_engine_apply_actions(oamd_engine* e, const int32_t* actions_dev) {
+    DeviceGuard dg(e->device);
+    launch_apply_actions(e->view(), actions_dev, e->stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_engine_selfplay_move(oamd_engine* e, const oamd_selfplay_config* cfg, int32_t* actions_dev,
+                              int32_t* finished_dev, float* features_dev, float* policy_dev) {
+    if (cfg->temperature_moves < 0 || !(cfg->temperature > 0.0f) || cfg->opening_moves < 0)
+        return fail(OAMD_INVALID_ARGUMENT, "bad self-play config");
+    if (cfg->emit_targets && (!features_dev || !policy_dev))
+        return fail(OAMD_INVALID_ARGUMENT, "emit_targets needs features and policy buffers");
+    SelfplayParams sp{cfg->temperature_moves, cfg->temperature, cfg->opening_moves, cfg->emit_targets};
+    DeviceGuard dg(e->device);
+    launch_selfplay_move(e->view(), sp, actions_dev, finished_dev, features_dev, policy_dev, e->stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_engine_random_openings(oamd_engine* e, int32_t max_moves, uint64_t seed) {
+    if (max_moves < 0) return fail(OAMD_INVALID_ARGUMENT, "max_moves must be >= 0");
+    DeviceGuard dg(e->device);
+    launch_random_openings(e->view(), max_moves, seed, e->stream);
+    LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_engine_game_key(oamd_engine* e, int32_t game, uint64_t* key) {
+    if (game < 0 || game >= e->G) return fail(OAMD_OUT_OF_RANGE, "game index out of range");
+    DeviceGuard dg(e->device);
+    HIPCHK(hipMemcpyAsync(key, &e->games[game].key, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return OAMD_OK;
+}
+
+}  // extern "C"

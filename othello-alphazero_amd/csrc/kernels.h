@@ -1,0 +1,63 @@
+// Launchers shared between the kernel translation units and the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/othello_mcts_amd.h"
+#include "bitboard.h"
+#include "engine.h"
+
+namespace oamd {
+
+struct SelfplayParams {
+    int32_t temperature_moves;
+    float temperature;
+    int32_t opening_moves;
+    int32_t emit_targets;
+};
+
+// tree.hip
+void launch_select(const EngineView& E, hipStream_t s);
+void launch_backup(const EngineView& E, hipStream_t s);
+void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s);
+void launch_set_evaluation(const EngineView& E, const float* pol, const float* val, int row_begin,
+                           int rows, hipStream_t s);
+void launch_leaf_flags(const EngineView& E, uint8_t* flags, hipStream_t s);
+void launch_reset(const EngineView& E, int game, uint64_t seed, hipStream_t s);
+void launch_apply_actions(const EngineView& E, const int32_t* actions, hipStream_t s);
+void launch_apply_one(const EngineView& E, int g, int action, hipStream_t s);
+void launch_root_stats(const EngineView& E, int game_begin, int n_games, oamd_root_info* info,
+                       int32_t* visits, float* q, int by_action, hipStream_t s);
+void launch_self_play_data(const EngineView& E, int g, float* feat, float* pol, hipStream_t s);
+void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int32_t* actions,
+                          int32_t* finished, float* feat, float* pol, hipStream_t s);
+void launch_random_openings(const EngineView& E, int max_moves, uint64_t seed, hipStream_t s);
+void launch_legal_moves(const uint64_t* me, const uint64_t* opp, uint64_t* out, int64_t n,
+                        hipStream_t s);
+void launch_flips(const uint64_t* mv, const uint64_t* me, const uint64_t* opp, uint64_t* out,
+                  int64_t n, hipStream_t s);
+void launch_apply_positions(const Pos* in, const int32_t* actions, Pos* out, int64_t n,
+                            hipStream_t s);
+
+// resnet.hip
+struct NetView {
+    int32_t cin;     // real input channels (1 + 2H)
+    int32_t C;       // conv channels
+    int32_t R;       // residual blocks
+    int32_t hidden;  // value head hidden units
+    int32_t dtype;   // oamd_dtype
+    const uint16_t* w;   // packed conv weights, all layers, fragment order
+    const float* bias;   // folded conv bias, (1 + 2R) * C
+    const float* head;   // head parameters, see resnet.hip
+};
+
+// features: packed engine rows (fw words per row, history H) or fp32 planes
+void launch_resnet_packed(const NetView& N, const uint64_t* feat, int fw, int H, int rows,
+                          float* policy, float* value, hipStream_t s);
+void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* policy, float* value,
+                       hipStream_t s);
+size_t resnet_packed_weight_elems(int C, int R);
+size_t resnet_head_floats(int C, int hidden);
+
+}  // namespace oamd

@@ -1,0 +1,813 @@
+// Search-tree kernels: one 64-lane wavefront per game.
+//
+// The reference runs num_threads CPU threads per game, each selecting
+// batch_size leaves under a mutex with virtual loss, sending them through the
+// NN and backing them up (search_thread.cpp:47-260). Here a whole game's step
+// (L = num_threads * batch_size leaves) is one wave of k_select, one row block
+// of the NN launch, and one wave of k_backup; all games of the engine run in
+// the same launches. Lanes parallelise what is parallel inside one game:
+// the child scan of PUCT (lane = child), virtual loss and backup (lane = path
+// depth), expansion (lane = square), feature gathers (lane = history slot).
+// The sequential dependence between the L descents (each sees the previous
+// descents' virtual losses) is kept exactly.
+//
+// Floating point: compiled with -ffp-contract=off and IEEE division/sqrt so
+// that every PUCT score, virtual loss and backup is bit-identical to the
+// reference's float arithmetic (search_thread.cpp:163-166, 198-249, 270-280).
+
+#include <hip/hip_runtime.h>
+
+#include "bitboard.h"
+#include "engine.h"
+#include "kernels.h"
+#include "rng.h"
+
+namespace oamd {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return v;
+}
+
+// First index of the maximum (strict '>' scan in child order, search_thread.cpp:222,254).
+__device__ __forceinline__ int wave_argmax_first(float v, int idx) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(v, off);
+        const int oi = __shfl_xor(idx, off);
+        if (ov > v || (ov == v && oi < idx)) {
+            v = ov;
+            idx = oi;
+        }
+    }
+    return idx;
+}
+
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__device__ __forceinline__ NodeStat load_stat(const NodeStat* s) {
+    const int4 v = *reinterpret_cast<const int4*>(s);
+    NodeStat r;
+    r.n = v.x;
+    r.w = __int_as_float(v.y);
+    r.q = __int_as_float(v.z);
+    r.p = __int_as_float(v.w);
+    return r;
+}
+
+__device__ __forceinline__ void store_stat(NodeStat* s, const NodeStat& r) {
+    *reinterpret_cast<int4*>(s) =
+        make_int4(r.n, __float_as_int(r.w), __float_as_int(r.q), __float_as_int(r.p));
+}
+
+__device__ __forceinline__ NodeLink load_link(const NodeLink* l) {
+    const int4 v = *reinterpret_cast<const int4*>(l);
+    return NodeLink{v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ void store_link(NodeLink* l, const NodeLink& v) {
+    *reinterpret_cast<int4*>(l) = make_int4(v.first_child, v.n_children, v.parent, v.player);
+}
+
+__device__ __forceinline__ Pos load_pos(const NodePos* p, int player) {
+    Pos r;
+    r.player = player;
+    r.pad_ = 0;
+    r.p1 = p->p1;
+    r.p2 = p->p2;
+    r.legal = p->legal;
+    r.next_legal = p->next_legal;
+    return r;
+}
+
+__device__ __forceinline__ void store_pos(NodePos* p, const Pos& v) {
+    p->p1 = v.p1;
+    p->p2 = v.p2;
+    p->legal = v.legal;
+    p->next_legal = v.next_legal;
+}
+
+// exploration_rate of search_thread.cpp:198-203, tabulated on the host with
+// the host's logf so that it is bit-identical to the CPU reference.
+__device__ __forceinline__ float explore_rate(const EngineView& E, int n) {
+    if (n >= 0 && n < kExploreTab) return E.explore_tab[n];
+    return logf(((float)(1 + n) + E.c_base) / E.c_base) + E.c_init;
+}
+
+__device__ __forceinline__ float sqrt_count(const EngineView& E, int n) {
+    if (n >= 0 && n < kExploreTab) return E.sqrt_tab[n];
+    return sqrtf((float)n);
+}
+
+// Square of the j-th legal action of a position (legal_actions order,
+// position.h:308-326), computed by lane = square.
+__device__ __forceinline__ int action_of_child(uint64_t legal, int j) {
+    if (legal == 0) return 64;
+    const int s = lane_id();
+    const bool set = (legal >> (63 - s)) & 1ULL;
+    const uint64_t before = s == 0 ? 0ULL : (legal & (~0ULL << (64 - s)));
+    const bool hit = set && popcount64(before) == j;
+    const uint64_t b = __ballot(hit);
+    return b ? (__ffsll((unsigned long long)b) - 1) : 64;
+}
+
+// Child index of an action in legal_actions order (mcts.cpp:147-153).
+__device__ __forceinline__ int child_index_of(uint64_t legal, int n_children, int action) {
+    if (action == 0 || n_children <= 1 || action == 64) return 0;
+    return popcount64(legal & (~0ULL << (64 - action)));
+}
+
+// Fill the packed features of row r: leaf = path[d]; ancestors continue into
+// the game history (position_iterator.h:24-71, transformation.h:83-116).
+__device__ __forceinline__ void write_packed_features(const EngineView& E, size_t base, int r,
+                                                      int d, int p0, int p1, int hist_node,
+                                                      int hist_n, int leaf_player, int t,
+                                                      bool valid) {
+    const int lane = lane_id();
+    uint64_t* row = E.feat + (size_t)r * E.FW;
+    // ancestor h = path[d - h] for h <= d, else hist[h - d - 1]
+    const int idx = d - lane;
+    const int from_p0 = __shfl(p0, idx & 63);
+    const int from_p1 = __shfl(p1, idx & 63);
+    const int hj = lane - d - 1;
+    const int from_h = __shfl(hist_node, hj & 63);
+    int anc = -1;
+    if (idx >= 0) anc = idx < 64 ? from_p0 : from_p1;
+    else if (hj < hist_n) anc = from_h;
+    uint64_t a1 = 0, a2 = 0;
+    if (lane < E.H && anc >= 0 && valid) {
+        const NodePos* np = E.pos + base + anc;
+        a1 = np->p1;
+        a2 = np->p2;
+    }
+    if (lane < E.H) {
+        row[2 + 2 * lane] = a1;
+        row[3 + 2 * lane] = a2;
+    }
+    if (lane == 0) {
+        const uint64_t meta = valid ? ((uint64_t)((leaf_player - 1) & 1) | ((uint64_t)t << 8) |
+                                       (1ULL << 16))
+                                    : 0ULL;
+        row[0] = meta;
+        row[1] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Selection: L descents with virtual loss (search_thread.cpp:59-100).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_select(EngineView E) {
+    const int g = blockIdx.x;
+    const int lane = lane_id();
+    GameState* gs = E.games + g;
+    const size_t base = (size_t)g * E.cap;
+    const int root = gs->root;
+    const int flags = gs->flags;
+    const uint64_t key = gs->key;
+    uint64_t event = gs->event;
+    const int hist_n = gs->hist_n;
+    const int hist_node = lane < 16 ? gs->hist[lane] : -1;
+    unsigned long long sims = 0, evals = 0;
+
+    for (int i = 0; i < E.L; ++i) {
+        const int r = g * E.L + i;
+        if (!(flags & kActive)) {
+            if (lane == 0) {
+                E.leaf[r] = -1;
+                E.depth[r] = 0;
+                E.trans[r] = 0;
+            }
+            write_packed_features(E, base, r, 0, 0, 0, -1, 0, 1, 0, false);
+            continue;
+        }
+        int node = root;
+        int d = 0;
+        int p0 = lane == 0 ? root : -1;  // path slot `lane`
+        int p1 = -1;                     // path slot 64 + lane
+        NodeLink lk = load_link(E.link + base + node);
+        while (!(lk.player == 0 || lk.n_children == 0) && d < kMaxDepth - 1) {
+            int child;
+            if (lk.n_children == 1) {
+                child = lk.first_child;  // search_thread.cpp:194-196
+            } else {
+                const int nc = lk.n_children, fc = lk.first_child;
+                const int parent_n = E.stat[base + node].n;
+                NodeStat cs{0, 0.0f, 0.0f, 0.0f};
+                if (lane < nc) cs = load_stat(E.stat + base + fc + lane);
+                const int total = wave_sum(lane < nc ? cs.n : 0);
+                const float mult = explore_rate(E, parent_n) * sqrt_count(E, total);
+                float prob = cs.p;
+                if (node == root && E.eps > 0.0f) {
+                    // fresh Dirichlet noise on every root selection (search_thread.cpp:230-249)
+                    float noise = 0.0f;
+                    if (lane < nc) noise = gamma_draw(stream_key(key, event, (uint32_t)lane), E.alpha);
+                    event += 1;
+                    float nsum = 0.0f;
+                    for (int j = 0; j < nc; ++j) nsum += readlane_f(noise, j);
+                    if (nsum == 0.0f) nsum = 1.0f;
+                    const float pm = 1.0f - E.eps;
+                    const float nm = E.eps / nsum;
+                    prob = cs.p * pm + noise * nm;
+                }
+                float ucb = cs.q + mult * prob / (1.0f + (float)cs.n);
+                if (lane >= nc) ucb = -__builtin_inff();
+                child = fc + wave_argmax_first(ucb, lane);
+            }
+            ++d;
+            if (lane == (d & 63)) {
+                if (d < 64) p0 = child;
+                else p1 = child;
+            }
+            node = child;
+            lk = load_link(E.link + base + node);
+        }
+        if (d == kMaxDepth - 1 && lk.player != 0 && lk.n_children != 0 && lane == 0)
+            atomicOr(&gs->flags, (int)kDepthCap);
+        // virtual loss on the path excluding the root (search_thread.cpp:69-76)
+        if (lane >= 1 && lane <= d) {
+            NodeStat s = load_stat(E.stat + base + p0);
+            s.n += 1;
+            s.w -= 1.0f;
+            s.q = s.w / (float)s.n;
+            store_stat(E.stat + base + p0, s);
+        }
+        if (64 + lane <= d) {
+            NodeStat s = load_stat(E.stat + base + p1);
+            s.n += 1;
+            s.w -= 1.0f;
+            s.q = s.w / (float)s.n;
+            store_stat(E.stat + base + p1, s);
+        }
+        if (lane == 0) E.stat[base + root].n += 1;  // search_thread.cpp:78
+        // record the path for the backup kernel
+        int* gp = E.path + (size_t)r * kMaxDepth;
+        if (lane <= d) gp[lane] = p0;
+        if (64 + lane <= d) gp[64 + lane] = p1;
+        const bool valid = lk.player != 0;
+        int t = 0;
+        if (valid) {
+            t = draw_transform(key, event);  // search_thread.cpp:92
+            event += 1;
+        }
+        if (lane == 0) {
+            E.leaf[r] = node;
+            E.depth[r] = d;
+            E.trans[r] = t;
+        }
+        write_packed_features(E, base, r, d, p0, p1, hist_node, hist_n, lk.player, t, valid);
+        sims += 1;
+        evals += valid ? 1 : 0;
+        wait_stores();
+    }
+    if (lane == 0) {
+        gs->event = event;
+        if (E.counters) {
+            atomicAdd(E.counters + 0, sims);
+            atomicAdd(E.counters + 1, evals);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Expansion + backup (search_thread.cpp:116-127, 130-190).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_backup(EngineView E) {
+    const int g = blockIdx.x;
+    const int lane = lane_id();
+    GameState* gs = E.games + g;
+    if (!(gs->flags & kActive)) return;
+    const size_t base = (size_t)g * E.cap;
+    const int root = gs->root;
+    int count = gs->count;
+    bool overflow = false;
+    __shared__ int expanded[kMaxLeaves];  // leaves expanded in this step, in order
+    int n_expanded = 0;
+
+    for (int i = 0; i < E.L; ++i) {
+        const int r = g * E.L + i;
+        const int leaf = E.leaf[r];
+        const int d = E.depth[r];
+        const int t = E.trans[r];
+        const NodeLink lk = load_link(E.link + base + leaf);
+        // duplicate leaves of one step expand once (search_thread.cpp:133-135)
+        bool hit = false;
+        for (int k = lane; k < n_expanded; k += 64) hit |= expanded[k] == leaf;
+        const bool already = __any(hit);
+        if (lk.player != 0 && lk.n_children == 0 && !already) {
+            const Pos P = load_pos(E.pos + base + leaf, lk.player);
+            const int nc = P.legal ? popcount64(P.legal) : 1;
+            if ((int64_t)count + nc > E.cap) {
+                overflow = true;  // leaf stays a leaf; value still backed up
+            } else {
+                const int fc = count;
+                count += nc;
+                const float* pol = E.policy + (size_t)r * 65;
+                int action = -1, j = 0;
+                if (P.legal) {
+                    const int s = lane;
+                    if ((P.legal >> (63 - s)) & 1ULL) {
+                        action = s;
+                        j = s == 0 ? 0 : popcount64(P.legal & (~0ULL << (64 - s)));
+                    }
+                } else if (lane == 0) {
+                    action = 64;
+                    j = 0;
+                }
+                if (action >= 0) {
+                    const Pos c = apply_action(P, action);
+                    const int id = fc + j;
+                    store_link(E.link + base + id, NodeLink{-1, 0, leaf, c.player});
+                    store_stat(E.stat + base + id,
+                               NodeStat{0, 0.0f, 0.0f, pol[transform_action(action, t)]});
+                    store_pos(E.pos + base + id, c);
+                }
+                if (lane == 0) store_link(E.link + base + leaf, NodeLink{fc, nc, lk.parent, lk.player});
+                if (lane == 0) expanded[n_expanded] = leaf;
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS write visible to the wave
+                __builtin_amdgcn_wave_barrier();
+                ++n_expanded;
+            }
+        }
+        if (d > 0) {
+            float v;
+            if (lk.player != 0) {
+                v = -E.value[r];
+            } else {
+                // terminal: score from the perspective of the parent's player
+                const NodeLink pl = load_link(E.link + base + lk.parent);
+                const NodePos lp = E.pos[base + leaf];
+                const uint64_t mine = pl.player == 1 ? lp.p1 : lp.p2;
+                const uint64_t theirs = pl.player == 1 ? lp.p2 : lp.p1;
+                const int a = popcount64(mine), b = popcount64(theirs);
+                v = a > b ? 1.0f : (a < b ? -1.0f : 0.0f);
+            }
+            const int* gp = E.path + (size_t)r * kMaxDepth;
+            // node at depth k receives v * (-1)^(d-k)  (sign flips walking up)
+            if (lane >= 1 && lane <= d) {
+                const int node = gp[lane];
+                const float vk = ((d - lane) & 1) ? -v : v;
+                NodeStat s = load_stat(E.stat + base + node);
+                s.w += 1.0f + vk;
+                s.q = s.w / (float)s.n;
+                store_stat(E.stat + base + node, s);
+            }
+            if (64 + lane <= d) {
+                const int k = 64 + lane;
+                const int node = gp[k];
+                const float vk = ((d - k) & 1) ? -v : v;
+                NodeStat s = load_stat(E.stat + base + node);
+                s.w += 1.0f + vk;
+                s.q = s.w / (float)s.n;
+                store_stat(E.stat + base + node, s);
+            }
+        }
+        wait_stores();
+    }
+    if (lane == 0) {
+        gs->count = count;
+        if (overflow) gs->flags |= kOverflow;
+    }
+    (void)root;
+}
+
+// ---------------------------------------------------------------------------
+// Packed -> fp32 features (B, 1+2H, 8, 8) for the external-evaluator path.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float plane_value(const uint64_t* row, int c, int sq_src) {
+    if (c == 0) return (float)(row[0] & 1ULL);
+    const uint64_t bb = row[1 + c];  // c = 1 + 2h -> word 2 + 2h; c = 2 + 2h -> 3 + 2h
+    return (float)((bb >> (63 - sq_src)) & 1ULL);
+}
+
+__global__ __launch_bounds__(256) void k_features_f32(EngineView E, float* out, int row_begin,
+                                                      int rows) {
+    const int rr = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (rr >= rows) return;
+    const int p = threadIdx.x & 63;
+    const uint64_t* row = E.feat + (size_t)(row_begin + rr) * E.FW;
+    const uint64_t meta = row[0];
+    const bool valid = (meta >> 16) & 1ULL;
+    const int t = (int)((meta >> 8) & 7ULL);
+    const int src = inverse_transform(p, t);
+    const int C = 1 + 2 * E.H;
+    float* o = out + (size_t)rr * C * 64;
+    for (int c = 0; c < C; ++c) o[c * 64 + p] = valid ? plane_value(row, c, src) : 0.0f;
+}
+
+__global__ __launch_bounds__(256) void k_set_evaluation(EngineView E, const float* policy,
+                                                        const float* value, int row_begin,
+                                                        int rows) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx < rows * 65) E.policy[(size_t)row_begin * 65 + idx] = policy[idx];
+    if (idx < rows) E.value[row_begin + idx] = value[idx];
+}
+
+__global__ __launch_bounds__(256) void k_leaf_flags(EngineView E, uint8_t* flags) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r < E.G * E.L) flags[r] = (uint8_t)((E.feat[(size_t)r * E.FW] >> 16) & 1ULL);
+}
+
+// ---------------------------------------------------------------------------
+// Game state: reset, moves, root statistics, self-play targets
+// ---------------------------------------------------------------------------
+__device__ void init_game(const EngineView& E, int g, uint64_t seed) {
+    GameState* gs = E.games + g;
+    const size_t base = (size_t)g * E.cap;
+    const Pos p = initial_position();
+    store_link(E.link + base, NodeLink{-1, 0, -1, p.player});
+    store_stat(E.stat + base, NodeStat{0, 0.0f, 0.0f, 1.0f});
+    store_pos(E.pos + base, p);
+    gs->root = 0;
+    gs->count = 1;
+    gs->flags = kActive;
+    gs->hist_n = 0;
+    gs->key = mix64(seed ^ mix64((uint64_t)g + 0x632BE59BD9B4E019ULL));
+    gs->event = 0;
+    gs->ply = 0;
+    for (int k = 0; k < 16; ++k) gs->hist[k] = -1;
+}
+
+__global__ void k_reset(EngineView E, int game, uint64_t seed) {
+    const int g = game >= 0 ? game : (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (g >= E.G || (game >= 0 && threadIdx.x + blockIdx.x != 0)) return;
+    init_game(E, g, seed);
+}
+
+// Move the root of game g along `action` (mcts.cpp:114-165): into the existing
+// child when the root is expanded, else into a fresh node. History = parents.
+__device__ void move_root(const EngineView& E, int g, int action) {
+    GameState* gs = E.games + g;
+    const size_t base = (size_t)g * E.cap;
+    const int root = gs->root;
+    const NodeLink lk = load_link(E.link + base + root);
+    int next;
+    if (lk.n_children == 0) {
+        if ((int64_t)gs->count + 1 > E.cap) {
+            gs->flags |= kOverflow;
+            return;
+        }
+        next = gs->count++;
+        const Pos p = load_pos(E.pos + base + root, lk.player);
+        const Pos c = apply_action(p, action);
+        store_link(E.link + base + next, NodeLink{-1, 0, root, c.player});
+        store_stat(E.stat + base + next, NodeStat{0, 0.0f, 0.0f, 1.0f});
+        store_pos(E.pos + base + next, c);
+    } else {
+        const uint64_t legal = E.pos[base + root].legal;
+        next = lk.first_child + child_index_of(legal, lk.n_children, action);
+    }
+    for (int k = 15; k > 0; --k) gs->hist[k] = gs->hist[k - 1];
+    gs->hist[0] = root;
+    gs->hist_n = gs->hist_n < 16 ? gs->hist_n + 1 : 16;
+    gs->root = next;
+    gs->ply += 1;
+}
+
+__global__ void k_apply_actions(EngineView E, const int32_t* actions) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= E.G) return;
+    const int a = actions[g];
+    if (a < 0 || !(E.games[g].flags & kActive)) return;
+    move_root(E, g, a);
+}
+
+__global__ void k_apply_one(EngineView E, int g, int action) { move_root(E, g, action); }
+
+// Root summary per game: info + visits/q indexed by action.
+__global__ __launch_bounds__(64) void k_root_stats(EngineView E, int game_begin,
+                                                   oamd_root_info* info, int32_t* visits,
+                                                   float* q, int by_action) {
+    const int g = game_begin + blockIdx.x;
+    const int lane = lane_id();
+    const GameState* gs = E.games + g;
+    const size_t base = (size_t)g * E.cap;
+    const int root = gs->root;
+    const NodeLink lk = load_link(E.link + base + root);
+    const NodePos rp = E.pos[base + root];
+    const int nc = lk.n_children;
+    int32_t* vo = visits + (size_t)blockIdx.x * 65;
+    float* qo = q + (size_t)blockIdx.x * 65;
+    if (by_action) {
+        // lane = square; pass in slot 64
+        vo[lane] = 0;
+        qo[lane] = 0.0f;
+        if (lane == 0) {
+            vo[64] = 0;
+            qo[64] = 0.0f;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (nc > 0) {
+            if (rp.legal) {
+                if ((rp.legal >> (63 - lane)) & 1ULL) {
+                    const int j = child_index_of(rp.legal, nc, lane);
+                    const NodeStat s = load_stat(E.stat + base + lk.first_child + j);
+                    vo[lane] = s.n;
+                    qo[lane] = s.q;
+                }
+            } else if (lane == 0) {
+                const NodeStat s = load_stat(E.stat + base + lk.first_child);
+                vo[64] = s.n;
+                qo[64] = s.q;
+            }
+        }
+    } else if (lane < nc) {
+        const NodeStat s = load_stat(E.stat + base + lk.first_child + lane);
+        vo[lane] = s.n;
+        qo[lane] = s.q;
+    }
+    if (lane == 0) {
+        oamd_root_info& I = info[blockIdx.x];
+        I.position.player = lk.player;
+        I.position.reserved = 0;
+        I.position.player1_discs = rp.p1;
+        I.position.player2_discs = rp.p2;
+        I.position.legal_moves = rp.legal;
+        I.position.next_legal_moves = rp.next_legal;
+        I.num_children = nc;
+        I.visit_count = E.stat[base + root].n;
+        I.overflow = (gs->flags & (kOverflow | kDepthCap)) ? gs->flags : 0;
+        I.reserved = 0;
+        I.node_count = gs->count;
+    }
+}
+
+// 8-fold self-play targets of the root (mcts.cpp:63-112): features of the root
+// under transform t (wave t of the block) and policy[transform(a,t)] = N_a/sum.
+__device__ void write_targets(const EngineView& E, int g, int t, float* feat_out, float* pol_out) {
+    const int lane = lane_id();
+    const GameState* gs = E.games + g;
+    const size_t base = (size_t)g * E.cap;
+    const int root = gs->root;
+    const NodeLink lk = load_link(E.link + base + root);
+    const NodePos rp = E.pos[base + root];
+    const int C = 1 + 2 * E.H;
+    float* fo = feat_out + (size_t)t * C * 64;
+    const int src = inverse_transform(lane, t);
+    fo[lane] = (float)(lk.player - 1);
+    for (int h = 0; h < E.H; ++h) {
+        int node = -1;
+        if (h == 0) node = root;
+        else if (h - 1 < gs->hist_n) node = gs->hist[h - 1];
+        float b = 0.0f, w = 0.0f;
+        if (node >= 0) {
+            const NodePos np = E.pos[base + node];
+            b = (float)((np.p1 >> (63 - src)) & 1ULL);
+            w = (float)((np.p2 >> (63 - src)) & 1ULL);
+        }
+        fo[(1 + 2 * h) * 64 + lane] = b;
+        fo[(2 + 2 * h) * 64 + lane] = w;
+    }
+    float* po = pol_out + (size_t)t * 65;
+    const int nc = lk.n_children;
+    int n = 0;
+    if (lane < nc) n = E.stat[base + lk.first_child + lane].n;
+    int sum = wave_sum(n);
+    if (sum == 0) sum = 1;
+    po[lane] = 0.0f;
+    if (lane == 0) po[64] = 0.0f;
+    __builtin_amdgcn_wave_barrier();
+    if (nc > 0) {
+        if (rp.legal) {
+            const int s = lane;
+            const bool set = (rp.legal >> (63 - s)) & 1ULL;
+            const int j = s == 0 ? 0 : popcount64(rp.legal & (~0ULL << (64 - s)));
+            const int nj = __shfl(n, j & 63);
+            if (set) po[transform_action(s, t)] = (float)nj / (float)sum;
+        } else if (lane == 0) {
+            po[64] = (float)n / (float)sum;
+        }
+    }
+}
+
+__global__ __launch_bounds__(512) void k_self_play_data(EngineView E, int g, float* feat_out,
+                                                        float* pol_out) {
+    write_targets(E, g, threadIdx.x >> 6, feat_out, pol_out);
+}
+
+// ---------------------------------------------------------------------------
+// On-device self-play move (train.py:404-452): choose, emit targets, apply,
+// restart finished games from a random opening.
+// ---------------------------------------------------------------------------
+__device__ void random_opening(const EngineView& E, int g, int max_moves) {
+    // lane-0 sequential: k ~ U{0..max_moves} uniformly random legal plies
+    GameState* gs = E.games + g;
+    if (max_moves <= 0) return;
+    const uint64_t ev = gs->event++;
+    const uint64_t key = stream_key(gs->key, ev, 0);
+    const int k = (int)(mix64(key) % (uint64_t)(max_moves + 1));
+    for (int m = 0; m < k; ++m) {
+        const size_t base = (size_t)g * E.cap;
+        const int root = gs->root;
+        const NodeLink lk = load_link(E.link + base + root);
+        if (lk.player == 0) break;
+        const NodePos rp = E.pos[base + root];
+        const int na = rp.legal ? popcount64(rp.legal) : 1;
+        const int pick = (int)(mix64(key + (uint64_t)(m + 1) * kGolden) % (uint64_t)na);
+        int action = 64;
+        if (rp.legal) {
+            uint64_t rem = rp.legal;
+            for (int s = 0, c = 0; s < 64; ++s) {
+                if ((rem >> (63 - s)) & 1ULL) {
+                    if (c == pick) {
+                        action = s;
+                        break;
+                    }
+                    ++c;
+                }
+            }
+        }
+        move_root(E, g, action);
+    }
+    gs->ply = 0;
+}
+
+__global__ void k_random_openings(EngineView E, int max_moves, uint64_t seed) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= E.G) return;
+    init_game(E, g, seed);
+    random_opening(E, g, max_moves);
+}
+
+__global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayParams sp,
+                                                      int32_t* actions, int32_t* finished,
+                                                      float* feat_out, float* pol_out) {
+    const int g = blockIdx.x;
+    const int lane = lane_id();
+    GameState* gs = E.games + g;
+    if (!(gs->flags & kActive)) {
+        if (lane == 0) {
+            if (actions) actions[g] = -1;
+            if (finished) finished[g] = 0;
+        }
+        return;
+    }
+    const size_t base = (size_t)g * E.cap;
+    const int root = gs->root;
+    const NodeLink lk = load_link(E.link + base + root);
+    const NodePos rp = E.pos[base + root];
+    const int nc = lk.n_children;
+    int action = -1;
+    if (lk.player != 0) {
+        const int na = rp.legal ? popcount64(rp.legal) : 1;
+        int n = 0;
+        if (lane < nc) n = E.stat[base + lk.first_child + lane].n;
+        const uint64_t ev = gs->event;
+        const float u = uniform(stream_key(gs->key, ev, 0), 0);
+        int j = 0;
+        if (nc == 0) {
+            j = (int)(u * (float)na);  // unexpanded root: uniform over legal actions
+            if (j >= na) j = na - 1;
+        } else if (gs->ply < sp.temperature_moves) {
+            // p ~ N^(1/temperature) (train.py:423-426); cdf search like numpy.random.choice
+            const float w = lane < nc ? powf((float)n, 1.0f / sp.temperature) : 0.0f;
+            float sum = 0.0f;
+            float cdf = 0.0f;
+            for (int k = 0; k < nc; ++k) {
+                sum += readlane_f(w, k);
+                if (k == lane) cdf = sum;
+            }
+            if (sum > 0.0f) {
+                const float target = u * sum;
+                const bool above = lane < nc && cdf > target;
+                const uint64_t b = __ballot(above);
+                j = b ? __ffsll((unsigned long long)b) - 1 : nc - 1;
+            } else {
+                j = (int)(u * (float)nc);
+                if (j >= nc) j = nc - 1;
+            }
+        } else {
+            // argmax with uniform random tie-break (train.py:428-430)
+            int m = n;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+            const uint64_t ties = __ballot(lane < nc && n == m);
+            const int nt = popcount64(ties);
+            int k = (int)(u * (float)nt);
+            if (k >= nt) k = nt - 1;
+            uint64_t rem = ties;
+            for (int x = 0; x < k; ++x) rem &= rem - 1;
+            j = __ffsll((unsigned long long)rem) - 1;
+        }
+        action = action_of_child(rp.legal, j);
+        if (sp.emit_targets && feat_out && nc > 0) {
+            const int C = 1 + 2 * E.H;
+            for (int t = 0; t < 8; ++t)
+                write_targets(E, g, t, feat_out + (size_t)g * 8 * C * 64, pol_out + (size_t)g * 8 * 65);
+        }
+        if (lane == 0) {
+            gs->event = ev + 1;
+            move_root(E, g, action);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    wait_stores();
+    int fin = 0;
+    if (lane == 0) {
+        const int r2 = gs->root;
+        const NodeLink l2 = load_link(E.link + base + r2);
+        if (l2.player == 0) {
+            const NodePos p2 = E.pos[base + r2];
+            const int b = popcount64(p2.p1), w = popcount64(p2.p2);
+            fin = b > w ? 2 : (b < w ? 3 : 1);  // 1 draw, 2 black won, 3 white won
+            const uint64_t key = gs->key;
+            const uint64_t ev = gs->event;
+            init_game(E, g, key ^ mix64(ev + 0xA5A5A5A5ULL));
+            random_opening(E, g, sp.opening_moves);
+        }
+        if (actions) actions[g] = action;
+        if (finished) finished[g] = fin;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Batched bitboards (position.h) — elementwise, one position per lane.
+// ---------------------------------------------------------------------------
+__global__ void k_legal_moves(const uint64_t* me, const uint64_t* opp, uint64_t* out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = legal_moves(me[i], opp[i]);
+}
+
+__global__ void k_flips(const uint64_t* mv, const uint64_t* me, const uint64_t* opp, uint64_t* out,
+                        int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = flips(mv[i], me[i], opp[i]);
+}
+
+__global__ void k_apply_positions(const Pos* in, const int32_t* actions, Pos* out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = apply_action(in[i], actions[i]);
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+void launch_select(const EngineView& E, hipStream_t s) {
+    hipLaunchKernelGGL(k_select, dim3(E.G), dim3(64), 0, s, E);
+}
+void launch_backup(const EngineView& E, hipStream_t s) {
+    hipLaunchKernelGGL(k_backup, dim3(E.G), dim3(64), 0, s, E);
+}
+void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s) {
+    if (rows > 0) hipLaunchKernelGGL(k_features_f32, dim3(blocks_for(rows, 4)), dim3(256), 0, s, E, out, row_begin, rows);
+}
+void launch_set_evaluation(const EngineView& E, const float* pol, const float* val, int row_begin,
+                           int rows, hipStream_t s) {
+    if (rows > 0)
+        hipLaunchKernelGGL(k_set_evaluation, dim3(blocks_for((int64_t)rows * 65, 256)), dim3(256), 0, s, E,
+                           pol, val, row_begin, rows);
+}
+void launch_leaf_flags(const EngineView& E, uint8_t* flags, hipStream_t s) {
+    hipLaunchKernelGGL(k_leaf_flags, dim3(blocks_for((int64_t)E.G * E.L, 256)), dim3(256), 0, s, E, flags);
+}
+void launch_reset(const EngineView& E, int game, uint64_t seed, hipStream_t s) {
+    if (game >= 0) hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, s, E, game, seed);
+    else hipLaunchKernelGGL(k_reset, dim3(blocks_for(E.G, 64)), dim3(64), 0, s, E, -1, seed);
+}
+void launch_apply_actions(const EngineView& E, const int32_t* actions, hipStream_t s) {
+    hipLaunchKernelGGL(k_apply_actions, dim3(blocks_for(E.G, 64)), dim3(64), 0, s, E, actions);
+}
+void launch_apply_one(const EngineView& E, int g, int action, hipStream_t s) {
+    hipLaunchKernelGGL(k_apply_one, dim3(1), dim3(1), 0, s, E, g, action);
+}
+void launch_root_stats(const EngineView& E, int game_begin, int n_games, oamd_root_info* info,
+                       int32_t* visits, float* q, int by_action, hipStream_t s) {
+    hipLaunchKernelGGL(k_root_stats, dim3(n_games), dim3(64), 0, s, E, game_begin, info, visits, q, by_action);
+}
+void launch_self_play_data(const EngineView& E, int g, float* feat, float* pol, hipStream_t s) {
+    hipLaunchKernelGGL(k_self_play_data, dim3(1), dim3(512), 0, s, E, g, feat, pol);
+}
+void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int32_t* actions,
+                          int32_t* finished, float* feat, float* pol, hipStream_t s) {
+    hipLaunchKernelGGL(k_selfplay_move, dim3(E.G), dim3(64), 0, s, E, sp, actions, finished, feat, pol);
+}
+void launch_random_openings(const EngineView& E, int max_moves, uint64_t seed, hipStream_t s) {
+    hipLaunchKernelGGL(k_random_openings, dim3(blocks_for(E.G, 64)), dim3(64), 0, s, E, max_moves, seed);
+}
+void launch_legal_moves(const uint64_t* me, const uint64_t* opp, uint64_t* out, int64_t n, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_legal_moves, dim3(blocks_for(n, 256)), dim3(256), 0, s, me, opp, out, n);
+}
+void launch_flips(const uint64_t* mv, const uint64_t* me, const uint64_t* opp, uint64_t* out, int64_t n,
+                  hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_flips, dim3(blocks_for(n, 256)), dim3(256), 0, s, mv, me, opp, out, n);
+}
+void launch_apply_positions(const Pos* in, const int32_t* actions, Pos* out, int64_t n, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(k_apply_positions, dim3(blocks_for(n, 256)), dim3(256), 0, s, in, actions, out, n);
+}
+
+}  // namespace oamd

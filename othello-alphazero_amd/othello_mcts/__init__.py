@@ -1,0 +1,37 @@
+"""MI355X-native drop-in for the reference's ``othello_mcts`` package.
+
+Same import surface as cpp/src/othello_mcts/__init__.py:1-6 (``MCTS``,
+``Position``, ``get_flips``, ``get_legal_moves``), backed by hand-written HIP
+kernels for gfx950 behind the C ABI in include/othello_mcts_amd.h. Additive
+API: ``BatchedMCTS`` (G games per GPU, on-device self-play driver) and
+``NativeNet`` (fused bf16/fp16 AlphaZeroNet forward).
+
+There is no CPU fallback: importing works anywhere the extension was built,
+but creating a search object needs a ROCm GPU and raises otherwise.
+"""
+
+# The reference imports torch first (its extension links libtorch). We keep the
+# same order so user code that relies on it behaves identically.
+import torch  # noqa: F401
+
+from ._othello_mcts_impl import (  # noqa: F401
+    MCTS,
+    Position,
+    SearchConfig,
+    abi_version,
+    device_count,
+    get_flips,
+    get_legal_moves,
+)
+from .batched import BatchedMCTS  # noqa: E402,F401
+from .native import NativeNet  # noqa: E402,F401
+
+__all__ = [
+    "MCTS",
+    "Position",
+    "get_flips",
+    "get_legal_moves",
+    "BatchedMCTS",
+    "NativeNet",
+    "SearchConfig",
+]

@@ -1,0 +1,134 @@
+"""Native AlphaZeroNet evaluation (fused HIP kernel, csrc/resnet.hip).
+
+``NativeNet`` packs a reference ``AlphaZeroNet`` state_dict
+(python/othello_alphazero/neural_net.py:138-172; keys listed in SURVEY.md §5)
+into the kernel's format: BatchNorm (eval, eps 1e-5) folded into each conv,
+weights in MFMA fragment order, bf16 (default) or fp16. It is itself a valid
+``NeuralNet`` callable (features -> {"policy", "value"}), and ``MCTS.search`` /
+``BatchedMCTS.search`` recognise it and run the whole search on the GPU with
+no Python in the loop.
+
+``resolve`` is what ``MCTS.search`` calls on the object it is given: an
+``AlphaZeroNet``-shaped module in eval mode (also behind ``torch.compile``) is
+converted once and cached; the cache is invalidated whenever a parameter or
+buffer is modified in place (tensor ``_version``), so a training loop that
+updates the net between self-play games is always searched with fresh
+weights. Set ``OTHELLO_MCTS_NATIVE_NN=0`` (or ``MCTS.set_native_nn(False)``)
+to always call the Python module instead (the reference's exact numerics).
+"""
+
+from __future__ import annotations
+
+import os
+import weakref
+
+import numpy as np
+import torch
+
+from ._othello_mcts_impl import _Net
+from .synthetic import net_config_from_state_dict
+
+_DTYPES = {"bf16": 0, "bfloat16": 0, "fp16": 1, "float16": 1}
+
+
+def _to_numpy_state(sd) -> dict[str, np.ndarray]:
+    out = {}
+    for k, v in sd.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().to("cpu", torch.float32).numpy()
+        out[k] = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
+    return out
+
+
+class NativeNet:
+    """Fused-kernel AlphaZeroNet on one GPU (eval mode only)."""
+
+    def __init__(self, net_or_state_dict, device: int | str | torch.device | None = None,
+                 dtype: str = "bf16") -> None:
+        if hasattr(net_or_state_dict, "state_dict"):
+            mod = getattr(net_or_state_dict, "_orig_mod", net_or_state_dict)
+            sd = mod.state_dict()
+        else:
+            sd = net_or_state_dict
+        self.config = net_config_from_state_dict(sd)
+        if dtype not in _DTYPES:
+            raise ValueError(f"dtype must be one of {sorted(_DTYPES)}, got {dtype!r}")
+        self.dtype = dtype
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device if isinstance(device, int) else torch.device(device).index or 0)
+        c = self.config
+        self._net = _Net(self.device.index, c["in_channels"], c["conv_channels"], c["num_residual_blocks"],
+                         c["value_head_hidden_channels"], _DTYPES[dtype])
+        self.load_state_dict(sd)
+
+    def load_state_dict(self, sd) -> None:
+        arrs = _to_numpy_state(sd)
+        tensors = []
+        for key, numel in self._net.state_keys():
+            a = arrs[key].reshape(-1)
+            if a.size != numel:
+                raise ValueError(f"{key}: expected {numel} elements, got {a.size}")
+            tensors.append(a)
+        self._net.load_state(tensors)
+
+    @property
+    def handle(self) -> int:
+        return self._net.handle
+
+    @property
+    def history_size(self) -> int:
+        return (self.config["in_channels"] - 1) // 2
+
+    def __call__(self, features: torch.Tensor) -> dict[str, torch.Tensor]:
+        x = features.to(self.device, torch.float32).contiguous()
+        rows = x.shape[0]
+        policy = torch.empty((rows, 65), dtype=torch.float32, device=self.device)
+        value = torch.empty((rows,), dtype=torch.float32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self._net.forward(x.data_ptr(), rows, policy.data_ptr(), value.data_ptr(), stream)
+        return {"policy": policy, "value": value}
+
+
+def _looks_like_alphazero(m) -> bool:
+    return all(hasattr(m, a) for a in ("conv_block", "residual_blocks", "policy_head", "value_head"))
+
+
+_cache: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _signature(m) -> tuple:
+    sig = []
+    for t in list(m.parameters()) + list(m.buffers()):
+        sig.append((t.data_ptr(), t._version))
+    return tuple(sig)
+
+
+def resolve(neural_net, device: int, history_size: int):
+    """NativeNet to use for ``neural_net`` on ``device``, or None (call it instead)."""
+    if isinstance(neural_net, NativeNet):
+        if neural_net.device.index != device:
+            raise ValueError(f"NativeNet lives on cuda:{neural_net.device.index}, the search on cuda:{device}")
+        if neural_net.history_size != history_size:
+            raise ValueError("NativeNet in_channels does not match 1 + 2 * history_size")
+        return neural_net
+    if os.environ.get("OTHELLO_MCTS_NATIVE_NN", "1") == "0":
+        return None
+    m = getattr(neural_net, "_orig_mod", neural_net)
+    if not isinstance(m, torch.nn.Module) or not _looks_like_alphazero(m) or m.training:
+        return None
+    try:
+        cfg = net_config_from_state_dict(m.state_dict())
+    except (KeyError, AttributeError):
+        return None
+    if cfg["conv_channels"] not in (128, 256) or cfg["in_channels"] != 1 + 2 * history_size:
+        return None
+    if cfg["num_squares"] != 64 or cfg["num_actions"] != 65:
+        return None
+    sig = _signature(m)
+    hit = _cache.get(m)
+    if hit is not None and hit[0] == sig and hit[1].device.index == device:
+        return hit[1]
+    nn_ = NativeNet(m, device=device)
+    _cache[m] = (sig, nn_)
+    return nn_

@@ -145,10 +145,12 @@ def make_strings_errors() -> None:
         f = line.split()
         if f[0] == "P":
             pend = [int(f[1]), f[2], f[3], f[4]]
+        elif f[0] == "Q":
+            pend.append([int(x) for x in f[1:]])
         else:
             s = bytes(int(x, 16) for x in f[1:]).decode("utf-8")
             out["strings"].append({"player": pend[0], "p1": pend[1], "p2": pend[2],
-                                   "legal": pend[3], "text": s})
+                                   "legal": pend[3], "actions": pend[4], "text": s})
     for line in run("errors"):
         _, name, kind, *msg = line.split(" ")
         out["errors"][name] = {"kind": kind, "message": " ".join(msg)}

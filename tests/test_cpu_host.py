@@ -1,0 +1,156 @@
+"""CPU-side checks of the product: the C-ABI library loads and exports every
+declared symbol, and the host Position API (same bitboard source as the
+kernels) reproduces the reference's golden vectors, strings and errors.
+No GPU compute is called here."""
+
+import ctypes
+import json
+import re
+
+import numpy as np
+import pytest
+
+from conftest import PKG, ROOT, gpu_available
+
+import othello_mcts as om
+from othello_mcts.synthetic import alphazero_state_dict, net_config_from_state_dict, random_opening_actions
+
+
+def u(x):
+    return int(np.int64(x).view(np.uint64))
+
+
+def test_abi_exports_every_declared_symbol():
+    header = (ROOT / "include" / "othello_mcts_amd.h").read_text()
+    names = set(re.findall(r"\b(oamd_[a-z0-9_]+)\s*\(", header))
+    assert len(names) > 30
+    lib = ctypes.CDLL(str(PKG / "othello_mcts" / "liboamd.so"))
+    missing = [n for n in sorted(names) if not hasattr(lib, n)]
+    assert not missing, missing
+    assert lib.oamd_abi_version() == 1
+
+
+def test_abi_device_count_without_gpu_is_safe():
+    lib = ctypes.CDLL(str(PKG / "othello_mcts" / "liboamd.so"))
+    n = ctypes.c_int32(-1)
+    assert lib.oamd_device_count(ctypes.byref(n)) == 0
+    assert n.value >= 0
+
+
+def test_package_surface_matches_reference():
+    # cpp/src/othello_mcts/__init__.py:6 exports these four names
+    for name in ("MCTS", "Position", "get_flips", "get_legal_moves"):
+        assert hasattr(om, name)
+    P = om.Position
+    for m in ("initial_position", "player", "player1_discs", "player2_discs", "__getitem__",
+              "legal_moves", "is_legal_move", "legal_actions", "apply_move", "apply_pass",
+              "apply_action", "is_terminal", "__str__"):
+        assert hasattr(P, m), m
+    for m in ("reset_position", "position", "search", "visit_counts", "mean_action_values",
+              "self_play_data", "apply_action", "history_size", "set_history_size", "torch_device",
+              "set_torch_device", "torch_pin_memory", "set_torch_pin_memory", "num_simulations",
+              "set_num_simulations", "num_threads", "set_num_threads", "batch_size", "set_batch_size",
+              "c_puct_base", "set_c_puct_base", "c_puct_init", "set_c_puct_init", "dirichlet_epsilon",
+              "set_dirichlet_epsilon", "dirichlet_alpha", "set_dirichlet_alpha"):
+        assert hasattr(om.MCTS, m), m
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure mode")
+def test_mcts_without_gpu_fails_loudly():
+    with pytest.raises(RuntimeError, match="needs a ROCm GPU"):
+        om.MCTS()
+
+
+@pytest.fixture(scope="module")
+def bb(golden_dir):
+    d = np.load(golden_dir / "bitboards.npz")
+    return {k: d[k] for k in d.files}
+
+
+def test_host_legal_moves_and_flips(bb):
+    for me, opp, legal in zip(bb["rnd_me"], bb["rnd_opp"], bb["rnd_legal"]):
+        assert om.get_legal_moves(u(me), u(opp)) == u(legal)
+    me, opp = bb["rnd_me"], bb["rnd_opp"]
+    for i, sq, fl in zip(bb["fl_index"], bb["fl_square"], bb["fl_flips"]):
+        assert om.get_flips(1 << (63 - int(sq)), u(me[i]), u(opp[i])) == u(fl)
+
+
+def test_host_position_replays_golden_games(bb):
+    player, p1, p2, legal = bb["pos_player"], bb["pos_p1"], bb["pos_p2"], bb["pos_legal"]
+    children = {}
+    for k, par in enumerate(bb["ch_parent"]):
+        children.setdefault(int(par), []).append(k)
+    # walk each game: position i+1 is a child of position i unless i is terminal
+    pos = om.Position.initial_position()
+    for i in range(len(player)):
+        exp = (int(player[i]), u(p1[i]), u(p2[i]), u(legal[i]))
+        assert (pos.player(), pos.player1_discs(), pos.player2_discs(), pos.legal_moves()) == exp
+        acts = pos.legal_actions()
+        assert acts == [int(bb["ch_action"][k]) for k in children.get(i, [])]
+        for k in children.get(i, []):
+            c = pos.apply_action(int(bb["ch_action"][k]))
+            assert (c.player(), c.player1_discs(), c.player2_discs(), c.legal_moves()) == (
+                int(bb["ch_player"][k]), u(bb["ch_p1"][k]), u(bb["ch_p2"][k]), u(bb["ch_legal"][k]))
+        if pos.is_terminal():
+            pos = om.Position.initial_position()
+        elif i + 1 < len(player):
+            nxt = (int(player[i + 1]), u(p1[i + 1]), u(p2[i + 1]))
+            for a in acts:
+                c = pos.apply_action(a)
+                if (c.player(), c.player1_discs(), c.player2_discs()) == nxt:
+                    pos = c
+                    break
+            else:
+                pytest.fail(f"position {i + 1} is not a child of {i}")
+
+
+def test_position_strings_and_errors(golden_dir):
+    g = json.loads((golden_dir / "strings_errors.json").read_text())
+    for rec in g["strings"]:
+        p = om.Position.initial_position()
+        for a in rec["actions"]:
+            p = p.apply_action(a)
+        assert (p.player(), f"{p.player1_discs():016x}", f"{p.player2_discs():016x}") == (
+            rec["player"], rec["p1"], rec["p2"])
+        assert str(p) == rec["text"]
+    err = g["errors"]
+    p = om.Position.initial_position()
+
+    def check(name, fn):
+        e = err[name]
+        exc = {"invalid_argument": ValueError, "out_of_range": IndexError}[e["kind"]]
+        with pytest.raises(exc) as ei:
+            fn()
+        assert str(ei.value) == e["message"]
+
+    check("at_-1", lambda: p[-1])
+    check("at_64", lambda: p[64])
+    check("is_legal_move_64", lambda: p.is_legal_move(64))
+    check("apply_action_65", lambda: p.apply_action(65))
+    check("apply_action_-1", lambda: p.apply_action(-1))
+    check("apply_action_0", lambda: p.apply_action(0))
+    check("apply_action_64", lambda: p.apply_action(64))
+    check("apply_pass", lambda: p.apply_pass())
+    check("apply_move_two_bits", lambda: p.apply_move(3))
+    check("apply_move_illegal", lambda: p.apply_move(1 << 63))
+
+
+def test_synthetic_state_dict_keys_and_config():
+    sd = alphazero_state_dict(3, 17, 128, 9, 128)
+    assert len(sd) == 153  # 153 keys for 128x10b
+    params = sum(v.size for k, v in sd.items() if not k.endswith(("running_mean", "running_var", "num_batches_tracked")))
+    assert params == 2_698_315  # SURVEY.md §6 (H=8)
+    assert net_config_from_state_dict(sd) == {"in_channels": 17, "num_squares": 64, "num_actions": 65,
+                                               "conv_channels": 128, "num_residual_blocks": 9,
+                                               "value_head_hidden_channels": 128}
+    again = alphazero_state_dict(3, 17, 128, 9, 128)
+    assert all(np.array_equal(sd[k], again[k]) for k in sd)
+
+
+def test_random_openings_are_legal():
+    for seed in range(50):
+        acts = random_opening_actions(seed, 8, om.Position)
+        assert len(acts) <= 8
+        p = om.Position.initial_position()
+        for a in acts:
+            p = p.apply_action(a)

@@ -1,0 +1,126 @@
+"""Native ResNet (csrc/resnet.hip) parity on the GPU.
+
+Yardsticks: the reference's own AlphaZeroNet outputs (tests/golden/resnet.npz,
+fp32 torch CPU) and the fp32 torch restatement (oracle/resnet_ref.py) on the
+same inputs. The kernel computes in bf16 (or fp16) with fp32 accumulation and
+fp32 heads; tolerances (absolute, on probabilities / tanh values):
+  bf16: policy <= 2e-3, value <= 3e-2;  fp16: policy <= 5e-4, value <= 6e-3.
+"""
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import resnet_ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+TOL = {"bf16": (2e-3, 3e-2), "fp16": (5e-4, 6e-3)}
+
+
+@pytest.fixture(scope="module")
+def om():
+    import othello_mcts
+
+    return othello_mcts
+
+
+def _sd(meta):
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    return alphazero_state_dict(meta["seed"], 1 + 2 * meta["history_size"], meta["conv_channels"],
+                                meta["num_residual_blocks"], meta["value_head_hidden_channels"])
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("name", ["c128b9_h8", "c128b9_h4", "c256b19_h8"])
+def test_native_net_vs_reference_golden(om, golden_dir, name, dtype):
+    meta = json.loads((golden_dir / "resnet_meta.json").read_text())[name]
+    g = np.load(golden_dir / "resnet.npz")
+    net = om.NativeNet(_sd(meta), device=0, dtype=dtype)
+    x = torch.from_numpy(g[f"{name}_x"].astype(np.float32)).to(DEV)
+    out = net(x)
+    torch.cuda.synchronize()
+    dp = np.abs(out["policy"].cpu().numpy() - g[f"{name}_policy"]).max()
+    dv = np.abs(out["value"].cpu().numpy() - g[f"{name}_value"]).max()
+    print(f"{name} {dtype}: max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e}")
+    tp, tv = TOL[dtype]
+    assert dp <= tp and dv <= tv
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("rows", [1, 3, 4, 5, 257, 2048])
+def test_native_net_vs_torch_fp32_restatement(om, rows, dtype):
+    """Ragged batch sizes (partial last workgroup tile) on real-looking planes."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    sd = alphazero_state_dict(99, 17, 128, 9, 128)
+    net = om.NativeNet(sd, device=0, dtype=dtype)
+    gen = torch.Generator().manual_seed(rows)
+    x = (torch.rand((rows, 17, 8, 8), generator=gen) < 0.3).float()
+    x[:, 0] = (torch.rand((rows, 1, 1), generator=gen) < 0.5).float()
+    x = x.to(DEV)
+    ref = resnet_ref.forward(sd, x)
+    out = net(x)
+    dp = (out["policy"] - ref["policy"]).abs().max().item()
+    dv = (out["value"] - ref["value"]).abs().max().item()
+    print(f"rows={rows} {dtype}: max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e}")
+    tp, tv = TOL[dtype]
+    assert dp <= tp and dv <= tv
+    torch.testing.assert_close(out["policy"].sum(1), torch.ones(rows, device=DEV), atol=1e-5, rtol=0)
+
+
+def test_native_search_equals_callback_search(om):
+    """The packed-feature native path and the fp32-feature callback path feed the
+    same kernel the same planes: visit counts must agree exactly."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    sd = alphazero_state_dict(7, 9, 128, 3, 64)
+    net = om.NativeNet(sd, device=0)
+    kw = dict(history_size=4, num_simulations=128, num_threads=2, batch_size=16, dirichlet_epsilon=0.25,
+              seed=21, node_capacity=1 << 16)
+    a = om.BatchedMCTS(8, **kw)
+    b = om.BatchedMCTS(8, **kw)
+    a.random_openings(6, seed=5)
+    b.random_openings(6, seed=5)
+
+    def cb(features):
+        return net(features)
+
+    for _ in range(3):
+        a.search(net)
+        b.search(cb)
+        for g in range(8):
+            assert a.visit_counts(g) == b.visit_counts(g)
+            assert a.mean_action_values(g) == b.mean_action_values(g)
+        out = a.selfplay_move(temperature_moves=0)
+        b.apply_actions(out["actions"])
+
+
+def test_mcts_autodetects_alphazero_module(om):
+    """MCTS.search(AlphaZeroNet-shaped module) runs the native path, refreshes
+    after in-place weight updates, and agrees with NativeNet."""
+    from othello_mcts import native
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    sd = alphazero_state_dict(8, 9, 128, 1, 32)
+
+    class Mod(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv_block = torch.nn.Module()
+            self.residual_blocks = torch.nn.Module()
+            self.policy_head = torch.nn.Module()
+            self.value_head = torch.nn.Module()
+            self.params = torch.nn.ParameterDict()
+            self._sd = {k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}
+
+        def state_dict(self, *a, **k):
+            return dict(self._sd)
+
+    m = Mod().eval()
+    nn1 = native.resolve(m, 0, 4)
+    assert nn1 is not None and native.resolve(m, 0, 4) is nn1
