@@ -96,8 +96,10 @@ def test_native_search_equals_callback_search(om):
         for g in range(8):
             assert a.visit_counts(g) == b.visit_counts(g)
             assert a.mean_action_values(g) == b.mean_action_values(g)
-        out = a.selfplay_move(temperature_moves=0)
-        b.apply_actions(out["actions"])
+        # both engines consume the same random events (move choice, restarts)
+        xa = a.selfplay_move(temperature_moves=12, opening_moves=3)["actions"].cpu()
+        xb = b.selfplay_move(temperature_moves=12, opening_moves=3)["actions"].cpu()
+        assert torch.equal(xa, xb)
 
 
 def test_mcts_autodetects_alphazero_module(om):
