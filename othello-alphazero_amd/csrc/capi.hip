@@ -471,7 +471,7 @@ int oamd_net_load_state(oamd_net* net, const float* const* t, int32_t n_tensors)
         }
         ks_global += (size_t)9 * CB;
     };
-    pack_conv(0, d.in_channels, 32);
+    pack_conv(0, d.in_channels, resnet_first_cin_pad());
     for (int i = 0; i < R; ++i) {
         pack_conv(1 + 2 * i, C, C);
         pack_conv(2 + 2 * i, C, C);

@@ -59,5 +59,6 @@ void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* pol
                        hipStream_t s);
 size_t resnet_packed_weight_elems(int C, int R);
 size_t resnet_head_floats(int C, int hidden);
+int resnet_first_cin_pad();  // first conv input channels after zero padding
 
 }  // namespace oamd

@@ -5,19 +5,21 @@
 //   * a 512-thread workgroup (8 waves, 2 per SIMD) owns BOARDS = 512/C boards
 //     (4 boards = 256 positions at C=128, 2 boards at C=256) and runs the whole
 //     tower + both heads on them; activations never leave LDS;
-//   * each 3x3 conv is an implicit GEMM  M = 64*BOARDS positions,
-//     N = C output channels, K = 9 taps x C_in, on v_mfma_f32_16x16x32_{bf16,f16};
-//     wave (wm, wn) owns the 64x64 output tile of board wm, columns wn*64..;
+//   * each 3x3 conv is an implicit GEMM  out[ch][pos] = W[ch][K] x X[K][pos],
+//     K = 9 taps x C_in, on v_mfma_f32_16x16x32_{bf16,f16} with the WEIGHTS as
+//     the A operand: an accumulator lane then holds 4 consecutive output
+//     channels of one position, so the epilogue writes 8 contiguous bytes;
+//     wave (wm, wn) owns 64 channels (wn) x 64 positions (board wm);
 //   * weights (BatchNorm folded, packed on the host in MFMA fragment order) are
-//     streamed once per workgroup per K-step (32 x C) through a 2-stage LDS
-//     ring with register staging, so L2 traffic is 1x per workgroup;
-//   * activations are bf16/fp16 in LDS, [position][channel] rows of 2C bytes
-//     with a 16-byte-chunk XOR swizzle (chunk ^ (row & 15)) so the 16 rows an
-//     MFMA A-fragment reads land in distinct LDS slots; zero padding of the
-//     3x3 taps at the board edge is a predicated load;
-//   * epilogue: + folded bias, (+ residual from LDS), ReLU, round to the
-//     activation dtype, written back in place (conv2 overwrites the block
-//     input element it just consumed as the skip);
+//     streamed once per workgroup through a 3-slot LDS ring by LDS-DMA
+//     (global_load_lds_dwordx4), one slot = one tap x 64 input channels; the
+//     slot for stage g+2 is issued while stage g computes, and the single
+//     barrier per stage sits between the two K=32 halves of the stage so the
+//     fragment reads of the next half always overlap MFMAs;
+//   * ONE activation buffer per workgroup, updated in place: [position][channel]
+//     rows of 2C bytes, 16-byte chunks XOR-swizzled by (row & 15) so the 16
+//     positions of an MFMA fragment hit distinct LDS slots; the residual skip
+//     is held in registers from conv1's epilogue to conv2's;
 //   * heads (1x1 convs, Linear layers, softmax(65), tanh) run in fp32 on VALU,
 //     one wave per (board, head).
 
@@ -32,10 +34,15 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int kThreads = 512;
+constexpr int kRing = 3;  // weight ring slots
+// LDS byte offset past any workgroup allocation (max 160 KiB): ds_read returns 0
+constexpr int kLdsZeroOff = 0x3FFF0;
 
-// Head parameter buffer layout (fp32), see pack in capi.hip.
+// Head parameter buffer layout (fp32), filled by oamd_net_load_state (capi.hip).
 struct HeadLayout {
     int pcw, pcb, vcw, vcb, plw, plb, v1w, v1b, v2w, v2b, total;
     __host__ __device__ HeadLayout(int C, int hidden) {
@@ -55,15 +62,17 @@ struct HeadLayout {
 
 size_t resnet_head_floats(int C, int hidden) { return (size_t)HeadLayout(C, hidden).total; }
 
-// K-steps: first conv 9 (C_in padded to 32), each tower conv 9 * C/32.
-__host__ __device__ inline int ksteps_first() { return 9; }
-__host__ __device__ inline int ksteps_tower(int C) { return 9 * (C / 32); }
+// A stage = one tap x 64 input channels = 2 K-steps of 32. The first conv's
+// input is zero-padded to 64 channels (9 stages), tower convs have 9 * C/64.
+__host__ __device__ inline int stages_first() { return 9; }
+__host__ __device__ inline int stages_tower(int C) { return 9 * (C / 64); }
 size_t resnet_packed_weight_elems(int C, int R) {
-    return (size_t)(ksteps_first() + 2 * R * ksteps_tower(C)) * 32 * C;
+    return (size_t)(stages_first() + 2 * R * stages_tower(C)) * 64 * C;
 }
+int resnet_first_cin_pad() { return 64; }
 
 template <int DT>
-__device__ __forceinline__ uint16_t to_act(float v) {
+__device__ __forceinline__ uint32_t to_act(float v) {
     if constexpr (DT == OAMD_BF16) {
         return __builtin_bit_cast(uint16_t, (__bf16)v);
     } else {
@@ -72,11 +81,11 @@ __device__ __forceinline__ uint16_t to_act(float v) {
 }
 
 template <int DT>
-__device__ __forceinline__ float from_act(uint16_t u) {
+__device__ __forceinline__ float from_act(uint32_t u) {
     if constexpr (DT == OAMD_BF16) {
-        return __uint_as_float((uint32_t)u << 16);
+        return __uint_as_float(u << 16);
     } else {
-        return (float)__builtin_bit_cast(_Float16, u);
+        return (float)__builtin_bit_cast(_Float16, (uint16_t)u);
     }
 }
 
@@ -91,183 +100,100 @@ __device__ __forceinline__ f32x4_t mfma(u32x4_t a, u32x4_t b, f32x4_t c) {
     }
 }
 
-// byte offset of (row, 8-channel chunk) in an activation buffer with rows of 2C bytes
+// byte offset of (row, 8-channel chunk) in the activation buffer (rows of 2C bytes)
 template <int C>
 __device__ __forceinline__ int act_chunk_off(int row, int chunk) {
     return row * (2 * C) + ((chunk ^ (row & 15)) << 4);
 }
 
-template <int C>
-__device__ __forceinline__ int act_elem_off(int row, int ch) {
-    return act_chunk_off<C>(row, ch >> 3) + ((ch & 7) << 1);
-}
-
 enum InputKind { kPacked = 0, kF32 = 1 };
 
-template <int C, int DT, int IN>
-__global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __restrict__ feat_in,
-                                                    int fw, int H, int rows,
-                                                    float* __restrict__ policy,
-                                                    float* __restrict__ value) {
-    constexpr int BOARDS = 512 / C;
-    constexpr int ROWS = BOARDS * 64;
-    constexpr int WN = 8 / BOARDS;      // waves along N
-    constexpr int ACT_BYTES = ROWS * C * 2;
-    constexpr int STAGE_BYTES = 32 * C * 2;
-    constexpr int STAGE_U4 = STAGE_BYTES / 16 / kThreads;  // uint4 per thread per stage
-    static_assert(STAGE_U4 >= 1, "stage too small");
+// Fragments of one K=32 step: 4 weight tiles (A: 16 channels x 32 K) and
+// 4 activation tiles (B: 32 K x 16 positions).
+struct Frags {
+    u32x4_t w[4];
+    u32x4_t x[4];
+};
 
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* act0 = smem;
-    unsigned char* act1 = smem + ACT_BYTES;
-    unsigned char* stage = smem + 2 * ACT_BYTES;
+template <int C>
+struct Geo {
+    static constexpr int BOARDS = 512 / C;
+    static constexpr int ROWS = BOARDS * 64;
+    static constexpr int WN = 8 / BOARDS;           // waves along output channels
+    static constexpr int ACT_BYTES = ROWS * C * 2;  // 64 KB for both C
+    static constexpr int STAGE_BYTES = 64 * C * 2;  // 16 KB (C=128) / 32 KB (C=256)
+    static constexpr int DMA_PER_THREAD = STAGE_BYTES / 16 / kThreads;
+    static constexpr int LDS = ACT_BYTES + kRing * STAGE_BYTES;
+};
 
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6;
-    const int lane = tid & 63;
-    const int wm = wave / WN;  // board of this wave
-    const int wn = wave % WN;
-    const int row0 = blockIdx.x * BOARDS;  // first board of the tile
-
-    // ---------------- input planes -> act1 (C_in padded to 32 channels) -------
-    if (tid < ROWS) {
-        const int b = tid >> 6, p = tid & 63;
-        const int gr = row0 + b;
-        uint16_t v[32];
-        const uint16_t one = to_act<DT>(1.0f);
-        if constexpr (IN == kPacked) {
-            uint32_t mask = 0;  // bit c = channel c is 1
-            if (gr < rows) {
-                const uint64_t* fr = reinterpret_cast<const uint64_t*>(feat_in) + (size_t)gr * fw;
-                const uint64_t meta = fr[0];
-                if ((meta >> 16) & 1ULL) {
-                    const int t = (int)((meta >> 8) & 7ULL);
-                    const int src = inverse_transform(p, t);
-                    mask = (uint32_t)(meta & 1ULL);
-                    for (int h = 0; h < H; ++h) {
-                        mask |= (uint32_t)((fr[2 + 2 * h] >> (63 - src)) & 1ULL) << (1 + 2 * h);
-                        mask |= (uint32_t)((fr[3 + 2 * h] >> (63 - src)) & 1ULL) << (2 + 2 * h);
-                    }
-                }
-            }
+// ds_read the fragments of K-step `sub` (0/1) of a stage.
+template <int C>
+__device__ __forceinline__ void load_frags(Frags& f, const unsigned char* act, const unsigned char* slot,
+                                           int sub, int cb64, const int (&xrow)[4], const bool (&xok)[4],
+                                           int wn, int lane) {
 #pragma unroll
-            for (int c = 0; c < 32; ++c) v[c] = ((mask >> c) & 1u) ? one : (uint16_t)0;
-        } else {
-            const float* fr = reinterpret_cast<const float*>(feat_in) + (size_t)gr * N.cin * 64;
-            const bool ok = gr < rows;
+    for (int n = 0; n < 4; ++n)
+        f.w[n] = *reinterpret_cast<const u32x4_t*>(slot + ((sub * (C / 16) + wn * 4 + n) * 64 + lane) * 16);
+    const int chunk = cb64 * 8 + sub * 4 + (lane >> 4);
 #pragma unroll
-            for (int c = 0; c < 32; ++c)
-                v[c] = (ok && c < N.cin) ? to_act<DT>(fr[c * 64 + p]) : (uint16_t)0;
-        }
-#pragma unroll
-        for (int ch = 0; ch < 4; ++ch) {
-            u32x4_t w;
-            w.x = (uint32_t)v[8 * ch + 0] | ((uint32_t)v[8 * ch + 1] << 16);
-            w.y = (uint32_t)v[8 * ch + 2] | ((uint32_t)v[8 * ch + 3] << 16);
-            w.z = (uint32_t)v[8 * ch + 4] | ((uint32_t)v[8 * ch + 5] << 16);
-            w.w = (uint32_t)v[8 * ch + 6] | ((uint32_t)v[8 * ch + 7] << 16);
-            *reinterpret_cast<u32x4_t*>(act1 + act_chunk_off<C>(tid, ch)) = w;
-        }
+    for (int m = 0; m < 4; ++m) {
+        // Off-board taps (the 3x3 zero padding) read beyond the workgroup's LDS
+        // allocation, which returns zeros: no data-dependent select, so the
+        // compiler never has to wait for these reads before the next MFMAs.
+        const int off = xok[m] ? act_chunk_off<C>(xrow[m], chunk) : kLdsZeroOff;
+        f.x[m] = *reinterpret_cast<const u32x4_t*>(act + off);
     }
+}
 
-    // ---------------- weight stream: register-staged 2-stage ring ------------
-    const u32x4_t* wg = reinterpret_cast<const u32x4_t*>(N.w);
-    const int total_ks = ksteps_first() + 2 * N.R * ksteps_tower(C);
-    u32x4_t wreg[STAGE_U4];
+template <int DT>
+__device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[4][4], const Frags& f) {
 #pragma unroll
-    for (int u = 0; u < STAGE_U4; ++u) wreg[u] = wg[(size_t)u * kThreads + tid];
+    for (int n = 0; n < 4; ++n)
 #pragma unroll
-    for (int u = 0; u < STAGE_U4; ++u)
-        *reinterpret_cast<u32x4_t*>(stage + ((size_t)u * kThreads + tid) * 16) = wreg[u];
-    __syncthreads();
+        for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
+}
 
-    f32x4_t acc[4][4];
+// positions (rows of the activation buffer) feeding tap (dy, dx) for the 4
+// position tiles of this lane; out-of-board taps read a valid row and zero it
+__device__ __forceinline__ void tap_rows(int tap, int wm, int lane, int (&xrow)[4], bool (&xok)[4]) {
+    const int dy = tap / 3 - 1, dx = tap % 3 - 1;
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-    int ks = 0;  // global K-step counter (drives the weight ring)
-    const int nlayers = 1 + 2 * N.R;
-    for (int layer = 0; layer < nlayers; ++layer) {
-        const bool first = layer == 0;
-        const bool conv2 = !first && ((layer - 1) & 1);
-        unsigned char* act_in = first ? act1 : (conv2 ? act1 : act0);
-        unsigned char* act_out = first ? act0 : (conv2 ? act0 : act1);
-        const int CB = first ? 1 : C / 32;
-
-        for (int tap = 0; tap < 9; ++tap) {
-            const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-            int a_row[4];
-            bool a_ok[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int s = m * 16 + (lane & 15);
-                const int yy = (s >> 3) + dy, xx = (s & 7) + dx;
-                a_ok[m] = (unsigned)yy < 8u && (unsigned)xx < 8u;
-                a_row[m] = wm * 64 + (a_ok[m] ? yy * 8 + xx : s);
-            }
-            for (int cb = 0; cb < CB; ++cb) {
-                // prefetch the next K-step's weights into registers
-                const bool more = ks + 1 < total_ks;
-                if (more) {
-#pragma unroll
-                    for (int u = 0; u < STAGE_U4; ++u)
-                        wreg[u] = wg[(size_t)(ks + 1) * (STAGE_BYTES / 16) + (size_t)u * kThreads + tid];
-                }
-                const unsigned char* st = stage + (ks & 1) * STAGE_BYTES;
-                u32x4_t a[4], b[4];
-                const int chunk = cb * 4 + (lane >> 4);
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const u32x4_t v =
-                        *reinterpret_cast<const u32x4_t*>(act_in + act_chunk_off<C>(a_row[m], chunk));
-                    a[m] = a_ok[m] ? v : u32x4_t{0u, 0u, 0u, 0u};
-                }
-#pragma unroll
-                for (int n = 0; n < 4; ++n)
-                    b[n] = *reinterpret_cast<const u32x4_t*>(st + (((wn * 4 + n) * 64) + lane) * 16);
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-#pragma unroll
-                    for (int n = 0; n < 4; ++n) acc[m][n] = mfma<DT>(a[m], b[n], acc[m][n]);
-                if (more) {
-#pragma unroll
-                    for (int u = 0; u < STAGE_U4; ++u)
-                        *reinterpret_cast<u32x4_t*>(stage + ((ks + 1) & 1) * STAGE_BYTES +
-                                                    ((size_t)u * kThreads + tid) * 16) = wreg[u];
-                }
-                __syncthreads();
-                ++ks;
-            }
-        }
-
-        // ---------------- epilogue: bias (+ skip) + ReLU -> act_out ------------
-        const float* bias = N.bias + (size_t)layer * C;
-        float bcol[4];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) bcol[n] = bias[wn * 64 + n * 16 + (lane & 15)];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                const int col = wn * 64 + n * 16 + (lane & 15);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int row = wm * 64 + m * 16 + (lane >> 4) * 4 + j;
-                    float v = acc[m][n][j] + bcol[n];
-                    const int off = act_elem_off<C>(row, col);
-                    if (conv2) v += from_act<DT>(*reinterpret_cast<const uint16_t*>(act0 + off));
-                    v = fmaxf(v, 0.0f);
-                    *reinterpret_cast<uint16_t*>(act_out + off) = to_act<DT>(v);
-                }
-                acc[m][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            }
-        }
-        __syncthreads();
+    for (int m = 0; m < 4; ++m) {
+        const int s = m * 16 + (lane & 15);
+        const int yy = (s >> 3) + dy, xx = (s & 7) + dx;
+        xok[m] = (unsigned)yy < 8u && (unsigned)xx < 8u;
+        xrow[m] = wm * 64 + (xok[m] ? yy * 8 + xx : s);
     }
+}
 
-    // ---------------- heads (fp32, VALU), final activations in act0 ---------
+template <int C>
+__device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsigned char* ring, int g,
+                                                int total, int tid) {
+    using G = Geo<C>;
+    if (g >= total) return;
+    const unsigned char* src = wsrc + (size_t)g * G::STAGE_BYTES;
+    unsigned char* dst = ring + (g % kRing) * G::STAGE_BYTES;
+    const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int i = 0; i < G::DMA_PER_THREAD; ++i) {
+        const int q = i * kThreads + wave * 64;  // first 16-byte chunk of this wave's piece
+        __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void wait_dma_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// all but the youngest stage's DMAs complete
+template <int C>
+__device__ __forceinline__ void wait_dma_stage() {
+    if constexpr (Geo<C>::DMA_PER_THREAD == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+}
+
+template <int C, int DT>
+__device__ void heads(const NetView& N, const unsigned char* act, int wave, int lane, int row0, int rows,
+                      float* __restrict__ policy, float* __restrict__ value) {
+    constexpr int BOARDS = Geo<C>::BOARDS;
     const HeadLayout HL(C, N.hidden);
     const float* hp = N.head;
     const int b = wave % BOARDS;
@@ -278,11 +204,11 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
         // policy head: 1x1 conv (C->2) + BN + ReLU, flatten c*64+s, Linear(128->65), softmax
         float h0 = hp[HL.pcb + 0], h1 = hp[HL.pcb + 1];
         for (int c8 = 0; c8 < C / 8; ++c8) {
-            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(act0 + act_chunk_off<C>(row, c8));
+            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(act + act_chunk_off<C>(row, c8));
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                const float x = from_act<DT>((uint16_t)(w4[e >> 1] >> ((e & 1) * 16)));
+                const float x = from_act<DT>((w4[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
                 h0 += x * hp[HL.pcw + c8 * 8 + e];
                 h1 += x * hp[HL.pcw + C + c8 * 8 + e];
             }
@@ -315,11 +241,11 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
         // value head: 1x1 conv (C->1) + BN + ReLU, Linear(64->hidden), ReLU, Linear(hidden->1), tanh
         float v = hp[HL.vcb];
         for (int c8 = 0; c8 < C / 8; ++c8) {
-            const u32x4_t q = *reinterpret_cast<const u32x4_t*>(act0 + act_chunk_off<C>(row, c8));
+            const u32x4_t q = *reinterpret_cast<const u32x4_t*>(act + act_chunk_off<C>(row, c8));
             const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                const float x = from_act<DT>((uint16_t)(w4[e >> 1] >> ((e & 1) * 16)));
+                const float x = from_act<DT>((w4[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
                 v += x * hp[HL.vcw + c8 * 8 + e];
             }
         }
@@ -343,24 +269,184 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
     }
 }
 
-template <int C>
-static size_t lds_bytes() {
-    return (size_t)2 * (512 / C) * 64 * C * 2 + 2 * 32 * C * 2;
+template <int C, int DT, int IN>
+__global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __restrict__ feat_in,
+                                                    int fw, int H, int rows,
+                                                    float* __restrict__ policy,
+                                                    float* __restrict__ value) {
+    using G = Geo<C>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* act = smem;
+    unsigned char* ring = smem + G::ACT_BYTES;
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int lane = tid & 63;
+    const int wm = wave / G::WN;  // board of this wave
+    const int wn = wave % G::WN;  // 64-channel block of this wave
+    const int row0 = blockIdx.x * G::BOARDS;
+    const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
+    const int total = stages_first() + 2 * N.R * stages_tower(C);
+
+    // weight stream starts right away (two stages ahead)
+    issue_stage_dma<C>(wsrc, ring, 0, total, tid);
+    issue_stage_dma<C>(wsrc, ring, 1, total, tid);
+
+    // ---------------- input planes -> act channels 0..63 ---------------------
+    if (tid < G::ROWS) {
+        const int b = tid >> 6, p = tid & 63;
+        const int gr = row0 + b;
+        const uint32_t one = to_act<DT>(1.0f);
+        uint32_t words[32];  // 64 channels as 16-bit pairs
+        if constexpr (IN == kPacked) {
+            uint32_t mask = 0;  // bit c = channel c is 1 (c < 31)
+            if (gr < rows) {
+                const uint64_t* fr = reinterpret_cast<const uint64_t*>(feat_in) + (size_t)gr * fw;
+                const uint64_t meta = fr[0];
+                if ((meta >> 16) & 1ULL) {
+                    const int t = (int)((meta >> 8) & 7ULL);
+                    const int src = inverse_transform(p, t);
+                    mask = (uint32_t)(meta & 1ULL);
+                    for (int h = 0; h < H; ++h) {
+                        mask |= (uint32_t)((fr[2 + 2 * h] >> (63 - src)) & 1ULL) << (1 + 2 * h);
+                        mask |= (uint32_t)((fr[3 + 2 * h] >> (63 - src)) & 1ULL) << (2 + 2 * h);
+                    }
+                }
+            }
+#pragma unroll
+            for (int w = 0; w < 32; ++w) {
+                const uint32_t lo = (w < 16 && ((mask >> (2 * w)) & 1u)) ? one : 0u;
+                const uint32_t hi = (w < 16 && ((mask >> (2 * w + 1)) & 1u)) ? one : 0u;
+                words[w] = lo | (hi << 16);
+            }
+        } else {
+            const float* fr = reinterpret_cast<const float*>(feat_in) + (size_t)gr * N.cin * 64;
+            const bool ok = gr < rows;
+#pragma unroll
+            for (int w = 0; w < 32; ++w) {
+                const int c0 = 2 * w, c1 = 2 * w + 1;
+                const uint32_t lo = (ok && c0 < N.cin) ? to_act<DT>(fr[c0 * 64 + p]) : 0u;
+                const uint32_t hi = (ok && c1 < N.cin) ? to_act<DT>(fr[c1 * 64 + p]) : 0u;
+                words[w] = lo | (hi << 16);
+            }
+        }
+#pragma unroll
+        for (int ch = 0; ch < 8; ++ch)
+            *reinterpret_cast<u32x4_t*>(act + act_chunk_off<C>(tid, ch)) =
+                u32x4_t{words[4 * ch], words[4 * ch + 1], words[4 * ch + 2], words[4 * ch + 3]};
+    }
+
+    f32x4_t acc[4][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[n][m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    u32x2_t skip[4][4];  // residual (block input) of this lane's 64 outputs
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) skip[n][m] = u32x2_t{0u, 0u};
+
+    Frags fa, fb;
+    int xrow[4];
+    bool xok[4];
+
+    // first stage of layer 0: its DMA and the input planes must be visible
+    wait_dma_all();
+    __syncthreads();
+    tap_rows(0, wm, lane, xrow, xok);
+    load_frags<C>(fa, act, ring, 0, 0, xrow, xok, wn, lane);
+
+    int g = 0;  // global stage index (weight ring position)
+    const int nlayers = 1 + 2 * N.R;
+    for (int layer = 0; layer < nlayers; ++layer) {
+        const int S = layer == 0 ? stages_first() : stages_tower(C);
+        const int per_tap = S / 9;  // 64-channel blocks per tap
+        float4 bv[4];               // folded bias of this lane's 16 output channels
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+            bv[n] = *reinterpret_cast<const float4*>(N.bias + (size_t)layer * C + wn * 64 + n * 16 +
+                                                     (lane >> 4) * 4);
+        // Stages 0..S-2 share one branch-free body (the waitcnt pass then counts
+        // the outstanding LDS reads exactly and never drains to lgkmcnt(0)).
+        int slot_i = g % kRing;
+        for (int s = 0; s + 1 < S; ++s, ++g) {
+            const int cb64 = s % per_tap;
+            const unsigned char* slot = ring + slot_i * G::STAGE_BYTES;
+            // second K-step of this stage; its reads overlap the first MFMAs
+            load_frags<C>(fb, act, slot, 1, cb64, xrow, xok, wn, lane);
+            mfma_frags<DT>(acc, fa);
+            // stage g+1 landed (issued one stage ago); stage g-1 drained by all waves
+            wait_dma_all();
+            __builtin_amdgcn_s_barrier();
+            issue_stage_dma<C>(wsrc, ring, g + 2, total, tid);
+            slot_i = slot_i == kRing - 1 ? 0 : slot_i + 1;
+            tap_rows((s + 1) / per_tap, wm, lane, xrow, xok);
+            load_frags<C>(fa, act, ring + slot_i * G::STAGE_BYTES, 0, (s + 1) % per_tap, xrow, xok, wn, lane);
+            mfma_frags<DT>(acc, fb);
+        }
+        {  // last stage of the layer
+            load_frags<C>(fb, act, ring + slot_i * G::STAGE_BYTES, 1, (S - 1) % per_tap, xrow, xok, wn, lane);
+            mfma_frags<DT>(acc, fa);
+            mfma_frags<DT>(acc, fb);
+            ++g;
+        }
+
+        // ---------------- epilogue: bias (+ skip) + ReLU, in place ------------
+        // g is now the first stage of the next layer (its DMA is in flight)
+        __syncthreads();  // every wave is done reading this layer's input and stage g-1
+        issue_stage_dma<C>(wsrc, ring, g + 1, total, tid);  // hidden behind the epilogue
+        const bool is_conv1 = layer > 0 && ((layer - 1) & 1) == 0;
+        const bool is_conv2 = layer > 0 && ((layer - 1) & 1) == 1;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int ch = wn * 64 + n * 16 + (lane >> 4) * 4;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int row = wm * 64 + m * 16 + (lane & 15);
+                const int off = act_chunk_off<C>(row, ch >> 3) + (ch & 7) * 2;
+                u32x2_t* p = reinterpret_cast<u32x2_t*>(act + off);
+                float v0 = acc[n][m][0] + bv[n].x, v1 = acc[n][m][1] + bv[n].y;
+                float v2 = acc[n][m][2] + bv[n].z, v3 = acc[n][m][3] + bv[n].w;
+                if (is_conv1) skip[n][m] = *p;  // block input, needed by conv2's epilogue
+                if (is_conv2) {
+                    const u32x2_t r = skip[n][m];
+                    v0 += from_act<DT>(r.x & 0xffffu);
+                    v1 += from_act<DT>(r.x >> 16);
+                    v2 += from_act<DT>(r.y & 0xffffu);
+                    v3 += from_act<DT>(r.y >> 16);
+                }
+                v0 = fmaxf(v0, 0.f);
+                v1 = fmaxf(v1, 0.f);
+                v2 = fmaxf(v2, 0.f);
+                v3 = fmaxf(v3, 0.f);
+                *p = u32x2_t{to_act<DT>(v0) | (to_act<DT>(v1) << 16), to_act<DT>(v2) | (to_act<DT>(v3) << 16)};
+                acc[n][m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        if (layer + 1 < nlayers) {
+            wait_dma_stage<C>();  // stage g has landed (stage g+1 may still fly)
+            __syncthreads();      // ... and this layer's output is complete
+            tap_rows(0, wm, lane, xrow, xok);
+            load_frags<C>(fa, act, ring + (g % kRing) * G::STAGE_BYTES, 0, 0, xrow, xok, wn, lane);
+        }
+    }
+    __syncthreads();
+    heads<C, DT>(N, act, wave, lane, row0, rows, policy, value);
 }
 
 template <int C, int DT, int IN>
 static void launch_t(const NetView& N, const void* feat, int fw, int H, int rows, float* pol,
                      float* val, hipStream_t s) {
-    constexpr int BOARDS = 512 / C;
-    const unsigned grid = (unsigned)((rows + BOARDS - 1) / BOARDS);
-    const size_t lds = lds_bytes<C>();
+    using G = Geo<C>;
+    const unsigned grid = (unsigned)((rows + G::BOARDS - 1) / G::BOARDS);
     static bool configured = false;
     if (!configured) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_resnet<C, DT, IN>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         configured = true;
     }
-    hipLaunchKernelGGL((k_resnet<C, DT, IN>), dim3(grid), dim3(kThreads), lds, s, N, feat, fw, H,
+    hipLaunchKernelGGL((k_resnet<C, DT, IN>), dim3(grid), dim3(kThreads), G::LDS, s, N, feat, fw, H,
                        rows, pol, val);
 }
 
