@@ -182,6 +182,10 @@ __global__ __launch_bounds__(64) void k_select(EngineView E) {
     const int hist_n = gs->hist_n;
     const int hist_node = lane < 16 ? gs->hist[lane] : -1;
     unsigned long long sims = 0, evals = 0;
+    // the root's link is fixed during selection (expansions happen in k_backup);
+    // its N grows by one per selected leaf (search_thread.cpp:78)
+    const NodeLink root_link = load_link(E.link + base + root);
+    int root_n = E.stat[base + root].n;
 
     for (int i = 0; i < E.L; ++i) {
         const int r = g * E.L + i;
@@ -198,18 +202,30 @@ __global__ __launch_bounds__(64) void k_select(EngineView E) {
         int d = 0;
         int p0 = lane == 0 ? root : -1;  // path slot `lane`
         int p1 = -1;                     // path slot 64 + lane
-        NodeLink lk = load_link(E.link + base + node);
+        NodeLink lk = root_link;
+        int node_n = root_n;  // visit count of `node` (parent N of the next choice)
+        // One dependent memory round trip per level: the stats AND links of all
+        // children are loaded together; the chosen child's link and N come from
+        // its lane (readlane), not from a second load.
         while (!(lk.player == 0 || lk.n_children == 0) && d < kMaxDepth - 1) {
             int child;
+            NodeLink clk;
+            int child_n;
             if (lk.n_children == 1) {
                 child = lk.first_child;  // search_thread.cpp:194-196
+                clk = load_link(E.link + base + child);
+                child_n = E.stat[base + child].n;
             } else {
                 const int nc = lk.n_children, fc = lk.first_child;
-                const int parent_n = E.stat[base + node].n;
+                const float er = explore_rate(E, node_n);
                 NodeStat cs{0, 0.0f, 0.0f, 0.0f};
-                if (lane < nc) cs = load_stat(E.stat + base + fc + lane);
+                NodeLink cl{0, 0, 0, 0};
+                if (lane < nc) {
+                    cs = load_stat(E.stat + base + fc + lane);
+                    cl = load_link(E.link + base + fc + lane);
+                }
                 const int total = wave_sum(lane < nc ? cs.n : 0);
-                const float mult = explore_rate(E, parent_n) * sqrt_count(E, total);
+                const float mult = er * sqrt_count(E, total);
                 float prob = cs.p;
                 if (node == root && E.eps > 0.0f) {
                     // fresh Dirichlet noise on every root selection (search_thread.cpp:230-249)
@@ -225,7 +241,11 @@ __global__ __launch_bounds__(64) void k_select(EngineView E) {
                 }
                 float ucb = cs.q + mult * prob / (1.0f + (float)cs.n);
                 if (lane >= nc) ucb = -__builtin_inff();
-                child = fc + wave_argmax_first(ucb, lane);
+                const int best = wave_argmax_first(ucb, lane);
+                child = fc + best;
+                clk = NodeLink{readlane_i(cl.first_child, best), readlane_i(cl.n_children, best),
+                               readlane_i(cl.parent, best), readlane_i(cl.player, best)};
+                child_n = readlane_i(cs.n, best);
             }
             ++d;
             if (lane == (d & 63)) {
@@ -233,7 +253,8 @@ __global__ __launch_bounds__(64) void k_select(EngineView E) {
                 else p1 = child;
             }
             node = child;
-            lk = load_link(E.link + base + node);
+            lk = clk;
+            node_n = child_n;
         }
         if (d == kMaxDepth - 1 && lk.player != 0 && lk.n_children != 0 && lane == 0)
             atomicOr(&gs->flags, (int)kDepthCap);
@@ -252,7 +273,8 @@ __global__ __launch_bounds__(64) void k_select(EngineView E) {
             s.q = s.w / (float)s.n;
             store_stat(E.stat + base + p1, s);
         }
-        if (lane == 0) E.stat[base + root].n += 1;  // search_thread.cpp:78
+        root_n += 1;
+        if (lane == 0) E.stat[base + root].n = root_n;  // search_thread.cpp:78
         // record the path for the backup kernel
         int* gp = E.path + (size_t)r * kMaxDepth;
         if (lane <= d) gp[lane] = p0;
