@@ -17,6 +17,8 @@
 
 using namespace oamd;
 
+constexpr int kMaxPipeline = 4;
+
 namespace {
 
 thread_local std::string g_err;
@@ -140,6 +142,12 @@ struct oamd_engine {
     // search state
     int steps_left = 0;
     int step_phase = 0;  // 0 = expect select, 1 = expect backup
+    // pipeline groups (0 = auto) and their streams / fork-join events
+    int pipeline = 0;
+    int n_pipe_streams = 0;
+    hipStream_t pipe_stream[kMaxPipeline] = {};
+    hipEvent_t fork_ev = nullptr;
+    hipEvent_t join_ev[kMaxPipeline] = {};
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev;
@@ -148,6 +156,17 @@ struct oamd_engine {
     int64_t nn_rows = 0;
 
     int L() const { return cfg.num_threads * cfg.batch_size; }
+
+    int ensure_streams(int K) {
+        if (K <= 1) return OAMD_OK;
+        if (!fork_ev) HIPCHK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+        while (n_pipe_streams < K) {
+            HIPCHK(hipStreamCreateWithFlags(&pipe_stream[n_pipe_streams], hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&join_ev[n_pipe_streams], hipEventDisableTiming));
+            ++n_pipe_streams;
+        }
+        return OAMD_OK;
+    }
     int FW() const { return feature_words(cfg.history_size); }
 
     EngineView view() const {
@@ -237,6 +256,11 @@ struct oamd_engine {
         dfree(q_dev);
         dfree(spd_dev);
         for (auto e : ev) (void)hipEventDestroy(e);
+        for (int k = 0; k < n_pipe_streams; ++k) {
+            (void)hipStreamDestroy(pipe_stream[k]);
+            (void)hipEventDestroy(join_ev[k]);
+        }
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
     }
 };
 
@@ -704,23 +728,51 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     const int steps = (e->cfg.num_simulations + L - 1) / L;
     const EngineView E = e->view();
     const NetView N = net->view();
-    const int rows = e->G * L;
+    // Pipeline groups: the games are split into K contiguous groups, each on its
+    // own stream, so one group's tree kernels (latency-bound, a wave per game)
+    // run while another group's ResNet launch owns the MFMA units. Games are
+    // independent, so the results are identical for every K.
+    int K = e->pipeline > 0 ? e->pipeline : (e->G >= 64 ? 2 : 1);
+    if (K > e->G) K = e->G;
+    if (K > kMaxPipeline) K = kMaxPipeline;
+    int rc = e->ensure_streams(K);
+    if (rc) return rc;
     if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
-    if (e->timing && (int)e->ev.size() < 2 * steps) {
-        while ((int)e->ev.size() < 2 * steps) {
-            hipEvent_t x;
-            HIPCHK(hipEventCreate(&x));
-            e->ev.push_back(x);
-        }
+    const int nev = 2 * steps * K;
+    while (e->timing && (int)e->ev.size() < nev) {
+        hipEvent_t x;
+        HIPCHK(hipEventCreate(&x));
+        e->ev.push_back(x);
+    }
+    hipStream_t st[kMaxPipeline];
+    int g0[kMaxPipeline], ng[kMaxPipeline];
+    for (int k = 0; k < K; ++k) {
+        g0[k] = (int)((int64_t)e->G * k / K);
+        ng[k] = (int)((int64_t)e->G * (k + 1) / K) - g0[k];
+        st[k] = K == 1 ? e->stream : e->pipe_stream[k];
+    }
+    if (K > 1) {  // fork from the caller's stream
+        HIPCHK(hipEventRecord(e->fork_ev, e->stream));
+        for (int k = 0; k < K; ++k) HIPCHK(hipStreamWaitEvent(st[k], e->fork_ev, 0));
     }
     for (int s = 0; s < steps; ++s) {
-        launch_select(E, e->stream);
-        if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * s], e->stream));
-        launch_resnet_packed(N, E.feat, E.FW, E.H, rows, E.policy, E.value, e->stream);
-        if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * s + 1], e->stream));
-        launch_backup(E, e->stream);
+        for (int k = 0; k < K; ++k) {
+            const size_t r0 = (size_t)g0[k] * L;
+            launch_select(E, st[k], g0[k], ng[k]);
+            if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * (s * K + k)], st[k]));
+            launch_resnet_packed(N, E.feat + r0 * E.FW, E.FW, E.H, ng[k] * L, E.policy + r0 * 65, E.value + r0,
+                                 st[k]);
+            if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * (s * K + k) + 1], st[k]));
+            launch_backup(E, st[k], g0[k], ng[k]);
+        }
     }
     LAUNCHCHK();
+    if (K > 1) {  // join back into the caller's stream
+        for (int k = 0; k < K; ++k) {
+            HIPCHK(hipEventRecord(e->join_ev[k], st[k]));
+            HIPCHK(hipStreamWaitEvent(e->stream, e->join_ev[k], 0));
+        }
+    }
     if (sims || evals || e->timing) {
         unsigned long long c[2] = {0, 0};
         if (sims || evals)
@@ -729,17 +781,24 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
         if (sims) *sims = (int64_t)c[0];
         if (evals) *evals = (int64_t)c[1];
         if (e->timing) {
-            for (int s = 0; s < steps; ++s) {
+            for (int i = 0; i < steps * K; ++i) {
                 float ms = 0.0f;
-                HIPCHK(hipEventElapsedTime(&ms, e->ev[2 * s], e->ev[2 * s + 1]));
+                HIPCHK(hipEventElapsedTime(&ms, e->ev[2 * i], e->ev[2 * i + 1]));
                 e->nn_ms += ms;
             }
-            e->nn_launches += steps;
-            e->nn_rows += (int64_t)steps * rows;
+            e->nn_launches += (int64_t)steps * K;
+            e->nn_rows += (int64_t)steps * e->G * L;
         }
     }
     e->step_phase = 0;
     e->steps_left = 0;
+    return OAMD_OK;
+}
+
+int oamd_engine_set_pipeline(oamd_engine* e, int32_t groups) {
+    if (groups < 0 || groups > kMaxPipeline)
+        return fail(OAMD_INVALID_ARGUMENT, "pipeline groups must be in [0, " + std::to_string(kMaxPipeline) + "]");
+    e->pipeline = groups;
     return OAMD_OK;
 }
 

@@ -18,8 +18,9 @@ struct SelfplayParams {
 };
 
 // tree.hip
-void launch_select(const EngineView& E, hipStream_t s);
-void launch_backup(const EngineView& E, hipStream_t s);
+// games [g0, g0 + ng) (ng < 0: to the end)
+void launch_select(const EngineView& E, hipStream_t s, int g0 = 0, int ng = -1);
+void launch_backup(const EngineView& E, hipStream_t s, int g0 = 0, int ng = -1);
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s);
 void launch_set_evaluation(const EngineView& E, const float* pol, const float* val, int row_begin,
                            int rows, hipStream_t s);

@@ -170,8 +170,8 @@ __device__ __forceinline__ void write_packed_features(const EngineView& E, size_
 // ---------------------------------------------------------------------------
 // Selection: L descents with virtual loss (search_thread.cpp:59-100).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_select(EngineView E) {
-    const int g = blockIdx.x;
+__global__ __launch_bounds__(64) void k_select(EngineView E, int g0) {
+    const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     GameState* gs = E.games + g;
     const size_t base = (size_t)g * E.cap;
@@ -307,8 +307,8 @@ __global__ __launch_bounds__(64) void k_select(EngineView E) {
 // ---------------------------------------------------------------------------
 // Expansion + backup (search_thread.cpp:116-127, 130-190).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_backup(EngineView E) {
-    const int g = blockIdx.x;
+__global__ __launch_bounds__(64) void k_backup(EngineView E, int g0) {
+    const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     GameState* gs = E.games + g;
     if (!(gs->flags & kActive)) return;
@@ -779,11 +779,13 @@ __global__ void k_apply_positions(const Pos* in, const int32_t* actions, Pos* ou
 // ---------------------------------------------------------------------------
 static inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-void launch_select(const EngineView& E, hipStream_t s) {
-    hipLaunchKernelGGL(k_select, dim3(E.G), dim3(64), 0, s, E);
+void launch_select(const EngineView& E, hipStream_t s, int g0, int ng) {
+    if (ng < 0) ng = E.G - g0;
+    if (ng > 0) hipLaunchKernelGGL(k_select, dim3(ng), dim3(64), 0, s, E, g0);
 }
-void launch_backup(const EngineView& E, hipStream_t s) {
-    hipLaunchKernelGGL(k_backup, dim3(E.G), dim3(64), 0, s, E);
+void launch_backup(const EngineView& E, hipStream_t s, int g0, int ng) {
+    if (ng < 0) ng = E.G - g0;
+    if (ng > 0) hipLaunchKernelGGL(k_backup, dim3(ng), dim3(64), 0, s, E, g0);
 }
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s) {
     if (rows > 0) hipLaunchKernelGGL(k_features_f32, dim3(blocks_for(rows, 4)), dim3(256), 0, s, E, out, row_begin, rows);

@@ -126,3 +126,24 @@ def test_mcts_autodetects_alphazero_module(om):
     m = Mod().eval()
     nn1 = native.resolve(m, 0, 4)
     assert nn1 is not None and native.resolve(m, 0, 4) is nn1
+
+
+def test_pipeline_groups_do_not_change_results(om):
+    """Splitting the games over 1, 2 or 3 stream groups is a pure scheduling
+    choice: every game's statistics must be identical."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(17, 9, 128, 2, 32), device=0)
+    kw = dict(history_size=4, num_simulations=96, num_threads=2, batch_size=8, seed=9,
+              node_capacity=1 << 15)
+    runs = []
+    for groups in (1, 2, 3):
+        b = om.BatchedMCTS(12, **kw)
+        b.engine.set_pipeline(groups)
+        b.random_openings(5, seed=3)
+        for _ in range(2):
+            b.search(net)
+            b.selfplay_move(temperature_moves=12, opening_moves=2)
+        b.search(net)
+        runs.append([(b.visit_counts(g), b.mean_action_values(g)) for g in range(12)])
+    assert runs[0] == runs[1] == runs[2]
