@@ -27,7 +27,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OAMD_ARCH", "gfx950")
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", str(CSRC), "-I", str(INCLUDE),
-          "-Wall", "-Wno-unused-function", "-fno-gpu-rdc"]
+          "-Wall", "-Wno-unused-function", "-fno-gpu-rdc", *os.environ.get("OAMD_EXTRA_FLAGS", "").split()]
 # tree.hip / rng.h / capi.hip tables must reproduce the reference's float
 # arithmetic bit for bit: no FMA contraction, IEEE division and sqrt.
 EXACT = ["-ffp-contract=off", "-fno-fast-math"]

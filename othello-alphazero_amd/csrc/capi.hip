@@ -147,6 +147,7 @@ struct oamd_engine {
     int n_pipe_streams = 0;
     hipStream_t pipe_stream[kMaxPipeline] = {};
     hipEvent_t fork_ev = nullptr;
+    hipEvent_t nn_token = nullptr;
     hipEvent_t join_ev[kMaxPipeline] = {};
     // timing
     bool timing = false;
@@ -160,6 +161,7 @@ struct oamd_engine {
     int ensure_streams(int K) {
         if (K <= 1) return OAMD_OK;
         if (!fork_ev) HIPCHK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+        if (!nn_token) HIPCHK(hipEventCreateWithFlags(&nn_token, hipEventDisableTiming));
         while (n_pipe_streams < K) {
             HIPCHK(hipStreamCreateWithFlags(&pipe_stream[n_pipe_streams], hipStreamNonBlocking));
             HIPCHK(hipEventCreateWithFlags(&join_ev[n_pipe_streams], hipEventDisableTiming));
@@ -261,6 +263,7 @@ struct oamd_engine {
             (void)hipEventDestroy(join_ev[k]);
         }
         if (fork_ev) (void)hipEventDestroy(fork_ev);
+        if (nn_token) (void)hipEventDestroy(nn_token);
     }
 };
 
@@ -463,9 +466,10 @@ int oamd_net_load_state(oamd_net* net, const float* const* t, int32_t n_tensors)
     std::vector<uint16_t> packed(resnet_packed_weight_elems(C, R));
     std::vector<float> bias((size_t)(1 + 2 * R) * C);
     size_t ks_global = 0;
-    // fold BN into a 3x3 conv and pack in MFMA B-fragment order:
-    // [ks = tap*CB + cb][ntile][lane][8], k_local = 8*(lane>>4)+j, n = ntile*16 + (lane&15)
-    auto pack_conv = [&](int layer, int cin, int cin_pad) {
+    // fold BN into a 3x3 conv and pack in MFMA A-fragment order, K-step by K-step
+    // (resnet_kstep): [ks][ntile][lane][8]; lane holds output channel
+    // ntile*16 + (lane&15) and input channels cb*32 + 8*chunk(lane>>4) + j
+    auto pack_conv = [&](int layer, int cin, bool first) {
         const float* W = t[ti++];
         const float* b = t[ti++];
         const float* g = t[ti++];
@@ -477,28 +481,29 @@ int oamd_net_load_state(oamd_net* net, const float* const* t, int32_t n_tensors)
             scale[n] = (double)g[n] / std::sqrt((double)var[n] + eps);
             bias[(size_t)layer * C + n] = (float)(((double)b[n] - (double)mu[n]) * scale[n] + (double)be[n]);
         }
-        const int CB = cin_pad / 32;
-        for (int tap = 0; tap < 9; ++tap) {
-            for (int cb = 0; cb < CB; ++cb) {
-                const size_t ks = ks_global + (size_t)tap * CB + cb;
-                for (int nt = 0; nt < C / 16; ++nt)
-                    for (int lane = 0; lane < 64; ++lane)
-                        for (int j = 0; j < 8; ++j) {
-                            const int ci = cb * 32 + 8 * (lane >> 4) + j;
-                            const int n = nt * 16 + (lane & 15);
-                            double v = 0.0;
-                            if (ci < cin) v = (double)W[((size_t)n * cin + ci) * 9 + tap] * scale[n];
-                            const size_t idx = (((ks * (C / 16) + nt) * 64) + lane) * 8 + j;
-                            packed[idx] = d.dtype == OAMD_BF16 ? f32_to_bf16_rne((float)v) : f32_to_f16((float)v);
-                        }
-            }
+        const int nk = resnet_ksteps(C, first);
+        for (int i = 0; i < nk; ++i) {
+            int tap, cb;
+            bool pad;
+            resnet_kstep(C, first, i, &tap, &cb, &pad);
+            const size_t ks = ks_global + (size_t)i;
+            for (int nt = 0; nt < C / 16; ++nt)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 8; ++j) {
+                        const int ci = cb * 32 + 8 * resnet_kgroup_chunk(lane >> 4) + j;
+                        const int n = nt * 16 + (lane & 15);
+                        double v = 0.0;
+                        if (!pad && ci < cin) v = (double)W[((size_t)n * cin + ci) * 9 + tap] * scale[n];
+                        const size_t idx = (((ks * (C / 16) + nt) * 64) + lane) * 8 + j;
+                        packed[idx] = d.dtype == OAMD_BF16 ? f32_to_bf16_rne((float)v) : f32_to_f16((float)v);
+                    }
         }
-        ks_global += (size_t)9 * CB;
+        ks_global += (size_t)nk;
     };
-    pack_conv(0, d.in_channels, resnet_first_cin_pad());
+    pack_conv(0, d.in_channels, true);
     for (int i = 0; i < R; ++i) {
-        pack_conv(1 + 2 * i, C, C);
-        pack_conv(2 + 2 * i, C, C);
+        pack_conv(1 + 2 * i, C, false);
+        pack_conv(2 + 2 * i, C, false);
     }
     // heads (fp32; 1x1 conv + BN folded)
     std::vector<float> head(resnet_head_floats(C, hid));
@@ -759,10 +764,15 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)g0[k] * L;
             launch_select(E, st[k], g0[k], ng[k]);
+            // NN launches of the groups run one after another (a token event):
+            // each owns all CUs' MFMA pipes while the other groups' tree
+            // kernels run beside it
+            if (K > 1 && (s > 0 || k > 0)) HIPCHK(hipStreamWaitEvent(st[k], e->nn_token, 0));
             if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * (s * K + k)], st[k]));
             launch_resnet_packed(N, E.feat + r0 * E.FW, E.FW, E.H, ng[k] * L, E.policy + r0 * 65, E.value + r0,
                                  st[k]);
             if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * (s * K + k) + 1], st[k]));
+            if (K > 1) HIPCHK(hipEventRecord(e->nn_token, st[k]));
             launch_backup(E, st[k], g0[k], ng[k]);
         }
     }

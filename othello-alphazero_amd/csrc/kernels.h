@@ -60,6 +60,13 @@ void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* pol
                        hipStream_t s);
 size_t resnet_packed_weight_elems(int C, int R);
 size_t resnet_head_floats(int C, int hidden);
-int resnet_first_cin_pad();  // first conv input channels after zero padding
+// Weight K-step schedule shared by the kernel and the host packer: a K-step is
+// one 3x3 tap x 32 input channels. K-steps per conv (first conv: input zero-
+// padded to 32 channels, 9 K-steps rounded up to whole weight stages with
+// zero-weight K-steps); tap and 32-channel block of K-step i (pad = all-zero).
+int resnet_ksteps(int C, bool first);
+void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad);
+// 8-channel chunk (0..3 within a K-step) that MFMA k-group kg (= lane >> 4) reads
+int resnet_kgroup_chunk(int kg);
 
 }  // namespace oamd

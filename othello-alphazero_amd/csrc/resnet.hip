@@ -3,27 +3,35 @@
 //
 // Work decomposition (DESIGN.md "ResNet kernel"):
 //   * a 512-thread workgroup (8 waves, 2 per SIMD) owns BOARDS = 512/C boards
-//     (4 boards = 256 positions at C=128, 2 boards at C=256) and runs the whole
-//     tower + both heads on them; activations never leave LDS;
+//     (4 boards at C=128, 2 boards at C=256) and runs the whole tower + both
+//     heads on them; activations never leave LDS;
 //   * each 3x3 conv is an implicit GEMM  out[ch][pos] = W[ch][K] x X[K][pos],
 //     K = 9 taps x C_in, on v_mfma_f32_16x16x32_{bf16,f16} with the WEIGHTS as
 //     the A operand: an accumulator lane then holds 4 consecutive output
 //     channels of one position, so the epilogue writes 8 contiguous bytes;
-//     wave (wm, wn) owns 64 channels (wn) x 64 positions (board wm);
-//   * weights (BatchNorm folded, packed on the host in MFMA fragment order) are
-//     streamed once per workgroup through a 3-slot LDS ring by LDS-DMA
-//     (global_load_lds_dwordx4), one slot = one tap x 64 input channels; the
-//     slot for stage g+2 is issued while stage g computes, and the single
-//     barrier per stage sits between the two K=32 halves of the stage so the
-//     fragment reads of the next half always overlap MFMAs;
-//   * ONE activation buffer per workgroup, updated in place: [position][channel]
-//     rows of 2C bytes, 16-byte chunks XOR-swizzled by (row & 15) so the 16
-//     positions of an MFMA fragment hit distinct LDS slots; the residual skip
-//     is held in registers from conv1's epilogue to conv2's;
+//     wave (wm, wn) owns 64 channels (wn) x the 64 positions of board wm;
+//   * K is walked in K-steps of one tap x 32 input channels. Weights (BatchNorm
+//     folded, packed on the host in fragment order) stream once per workgroup
+//     through a 3-slot LDS ring by LDS-DMA (global_load_lds_dwordx4); a 16 KiB
+//     slot holds one stage = 256/C K-steps. The slot for stage g+2 is issued at
+//     the barrier that opens stage g+1, so fragment reads always overlap MFMAs;
+//   * ONE activation buffer per workgroup, updated in place: each board is a
+//     zero-bordered 10x10 grid of rows of 2C+16 bytes ([position][channel]).
+//     The border makes every 3x3 tap read `lane base + uniform offset` (no
+//     per-read address arithmetic, no masking), and with the 16-byte row pad,
+//     the position->lane map kTilePos and the k-group->chunk map kgroup_chunk
+//     the 16 lanes of every ds_read_b128 lane group hit 16 distinct LDS slots
+//     for every tap (verified exhaustively in tests/test_cpu_host.py);
+//   * accumulators start from the folded bias (+ the residual skip for the
+//     second conv of a block, carried in registers from the first conv's
+//     epilogue), so the epilogue is cvt_pk + packed-i16 ReLU + one ds_write_b64;
 //   * heads (1x1 convs, Linear layers, softmax(65), tanh) run in fp32 on VALU,
 //     one wave per (board, head).
 
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <type_traits>
 
 #include "bitboard.h"
 #include "kernels.h"
@@ -32,15 +40,18 @@ namespace oamd {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) short i16x2_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int kThreads = 512;
-constexpr int kRing = 3;  // weight ring slots
-// LDS byte offset past any workgroup allocation (max 160 KiB): ds_read returns 0
-constexpr int kLdsZeroOff = 0x3FFF0;
+constexpr int kRing = 3;         // weight ring slots
+constexpr int kStageBytes = 16384;
 
 // Head parameter buffer layout (fp32), filled by oamd_net_load_state (capi.hip).
 struct HeadLayout {
@@ -62,14 +73,71 @@ struct HeadLayout {
 
 size_t resnet_head_floats(int C, int hidden) { return (size_t)HeadLayout(C, hidden).total; }
 
-// A stage = one tap x 64 input channels = 2 K-steps of 32. The first conv's
-// input is zero-padded to 64 channels (9 stages), tower convs have 9 * C/64.
-__host__ __device__ inline int stages_first() { return 9; }
-__host__ __device__ inline int stages_tower(int C) { return 9 * (C / 64); }
-size_t resnet_packed_weight_elems(int C, int R) {
-    return (size_t)(stages_first() + 2 * R * stages_tower(C)) * 64 * C;
+// ---- K-step schedule (shared with the host packer) --------------------------
+__host__ __device__ constexpr int ksteps_per_stage(int C) { return kStageBytes / (32 * C * 2); }
+__host__ __device__ constexpr int ksteps_first(int C) {
+    return (9 + ksteps_per_stage(C) - 1) / ksteps_per_stage(C) * ksteps_per_stage(C);
 }
-int resnet_first_cin_pad() { return 64; }
+__host__ __device__ constexpr int ksteps_tower(int C) { return 9 * (C / 32); }
+__host__ __device__ constexpr int kgroup_chunk(int kg) { return ((kg & 1) << 1) | (kg >> 1); }
+
+int resnet_ksteps(int C, bool first) { return first ? ksteps_first(C) : ksteps_tower(C); }
+void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad) {
+    if (first) {
+        *tap = i < 9 ? i : 8;
+        *cb = 0;
+        *pad = i >= 9;
+    } else {
+        *tap = i / (C / 32);
+        *cb = i % (C / 32);
+        *pad = false;
+    }
+}
+int resnet_kgroup_chunk(int kg) { return kgroup_chunk(kg); }
+size_t resnet_packed_weight_elems(int C, int R) {
+    return (size_t)(ksteps_first(C) + 2 * R * ksteps_tower(C)) * 32 * C;
+}
+
+// ---- activation layout --------------------------------------------------------
+// padded row of board position p = 8y + x inside its board's 10x10 grid
+__host__ __device__ constexpr int pad_row(int p) { return ((p >> 3) + 1) * 10 + (p & 7) + 1; }
+
+// kTilePos.p[16m + n]: board position held by B-fragment column n of position
+// tile m. Tile m takes, for every residue r = pad_row mod 16 (each residue
+// occurs exactly 4 times on the 8x8 board), the m-th position of that residue;
+// columns n in {0-3, 12-15} carry the odd residues, n in {4-11} the even ones.
+// With chunk offsets kgroup_chunk = {0,2,1,3} every ds_read_b128 lane group
+// then covers the 16 slots of a 256-byte bank row exactly once.
+struct TilePos {
+    unsigned char p[64];
+};
+constexpr TilePos make_tile_pos() {
+    TilePos t{};
+    for (int n = 0; n < 16; ++n) {
+        const int k = n < 4 ? n : (n < 12 ? n - 4 : n - 8);
+        const int r = (n < 4 || n >= 12) ? 2 * k + 1 : 2 * k;
+        int m = 0;
+        for (int p = 0; p < 64; ++p)
+            if (pad_row(p) % 16 == r) t.p[16 * (m++) + n] = (unsigned char)p;
+    }
+    return t;
+}
+__constant__ TilePos kTilePos = make_tile_pos();
+
+template <int C>
+struct Geo {
+    static constexpr int BOARDS = 512 / C;
+    static constexpr int WN = 8 / BOARDS;       // waves along output channels
+    static constexpr int RP = 2 * C + 16;       // row pitch (bytes)
+    static constexpr int BROWS = 100;           // 10x10 padded board
+    static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
+    static constexpr int KS = ksteps_per_stage(C);
+    static constexpr int KSTEP_BYTES = 32 * C * 2;
+    static constexpr int DMA_PER_THREAD = kStageBytes / 16 / kThreads;
+    static constexpr int LDS = ACT_BYTES + kRing * kStageBytes;
+    static_assert(LDS <= 160 * 1024, "LDS budget");
+    static_assert(DMA_PER_THREAD == 2, "wait_dma_stage assumes 2 DMAs per thread per stage");
+};
 
 template <int DT>
 __device__ __forceinline__ uint32_t to_act(float v) {
@@ -89,6 +157,19 @@ __device__ __forceinline__ float from_act(uint32_t u) {
     }
 }
 
+// relu(round(a)), relu(round(b)) packed: v_cvt_pk_{bf16,f16}_f32 (RNE) + v_pk_max_i16
+// (a 16-bit float is negative exactly when its bit pattern is a negative i16)
+template <int DT>
+__device__ __forceinline__ uint32_t pack_relu(float a, float b) {
+    i16x2_t s;
+    if constexpr (DT == OAMD_BF16) {
+        s = __builtin_bit_cast(i16x2_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+    } else {
+        s = __builtin_bit_cast(i16x2_t, __builtin_convertvector((f32x2_t){a, b}, f16x2_t));
+    }
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(s, (i16x2_t){0, 0}));
+}
+
 template <int DT>
 __device__ __forceinline__ f32x4_t mfma(u32x4_t a, u32x4_t b, f32x4_t c) {
     if constexpr (DT == OAMD_BF16) {
@@ -100,49 +181,44 @@ __device__ __forceinline__ f32x4_t mfma(u32x4_t a, u32x4_t b, f32x4_t c) {
     }
 }
 
-// byte offset of (row, 8-channel chunk) in the activation buffer (rows of 2C bytes)
-template <int C>
-__device__ __forceinline__ int act_chunk_off(int row, int chunk) {
-    return row * (2 * C) + ((chunk ^ (row & 15)) << 4);
-}
-
 enum InputKind { kPacked = 0, kF32 = 1 };
 
-// Fragments of one K=32 step: 4 weight tiles (A: 16 channels x 32 K) and
+// Fragments of one K-step: 4 weight tiles (A: 16 channels x 32 K) and
 // 4 activation tiles (B: 32 K x 16 positions).
 struct Frags {
     u32x4_t w[4];
     u32x4_t x[4];
 };
 
+// uniform byte offset of K-step i's rows/channels relative to the lane bases
 template <int C>
-struct Geo {
-    static constexpr int BOARDS = 512 / C;
-    static constexpr int ROWS = BOARDS * 64;
-    static constexpr int WN = 8 / BOARDS;           // waves along output channels
-    static constexpr int ACT_BYTES = ROWS * C * 2;  // 64 KB for both C
-    static constexpr int STAGE_BYTES = 64 * C * 2;  // 16 KB (C=128) / 32 KB (C=256)
-    static constexpr int DMA_PER_THREAD = STAGE_BYTES / 16 / kThreads;
-    static constexpr int LDS = ACT_BYTES + kRing * STAGE_BYTES;
-};
-
-// ds_read the fragments of K-step `sub` (0/1) of a stage.
-template <int C>
-__device__ __forceinline__ void load_frags(Frags& f, const unsigned char* act, const unsigned char* slot,
-                                           int sub, int cb64, const int (&xrow)[4], const bool (&xok)[4],
-                                           int wn, int lane) {
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-        f.w[n] = *reinterpret_cast<const u32x4_t*>(slot + ((sub * (C / 16) + wn * 4 + n) * 64 + lane) * 16);
-    const int chunk = cb64 * 8 + sub * 4 + (lane >> 4);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        // Off-board taps (the 3x3 zero padding) read beyond the workgroup's LDS
-        // allocation, which returns zeros: no data-dependent select, so the
-        // compiler never has to wait for these reads before the next MFMAs.
-        const int off = xok[m] ? act_chunk_off<C>(xrow[m], chunk) : kLdsZeroOff;
-        f.x[m] = *reinterpret_cast<const u32x4_t*>(act + off);
+__device__ __forceinline__ int kstep_offset(int i, bool first) {
+    int tap, cb;
+    if (first) {
+        tap = i < 9 ? i : 8;
+        cb = 0;
+    } else {
+        tap = i / (C / 32);
+        cb = i % (C / 32);
     }
+    const int dy = tap / 3 - 1, dx = tap - 3 * (tap / 3) - 1;
+    return (dy * 10 + dx) * Geo<C>::RP + cb * 64;
+}
+
+// ds_read the fragments of one K-step: wk = its weights in the ring (uniform),
+// aoff = kstep_offset (uniform); rd[m] / wl are per-lane bases
+template <int ABL = 0>
+__device__ __forceinline__ void load_frags(Frags& f, const unsigned char* act, const unsigned char* wk,
+                                           int aoff, const int (&rd)[4], int wl) {
+    if constexpr (!(ABL & 4)) {
+        const unsigned char* wp = wk + wl;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) f.w[n] = *reinterpret_cast<const u32x4_t*>(wp + n * 1024);
+    }
+    if constexpr (ABL & 2) return;
+    const unsigned char* ap = act + aoff;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) f.x[m] = *reinterpret_cast<const u32x4_t*>(ap + rd[m]);
 }
 
 template <int DT>
@@ -153,58 +229,39 @@ __device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[4][4], const Frags& f)
         for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
 }
 
-// positions (rows of the activation buffer) feeding tap (dy, dx) for the 4
-// position tiles of this lane; out-of-board taps read a valid row and zero it
-__device__ __forceinline__ void tap_rows(int tap, int wm, int lane, int (&xrow)[4], bool (&xok)[4]) {
-    const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int s = m * 16 + (lane & 15);
-        const int yy = (s >> 3) + dy, xx = (s & 7) + dx;
-        xok[m] = (unsigned)yy < 8u && (unsigned)xx < 8u;
-        xrow[m] = wm * 64 + (xok[m] ? yy * 8 + xx : s);
-    }
-}
-
-template <int C>
-__device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsigned char* ring, int g,
+__device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsigned char* ring, int g, int slot,
                                                 int total, int tid) {
-    using G = Geo<C>;
     if (g >= total) return;
-    const unsigned char* src = wsrc + (size_t)g * G::STAGE_BYTES;
-    unsigned char* dst = ring + (g % kRing) * G::STAGE_BYTES;
+    const unsigned char* src = wsrc + (size_t)g * kStageBytes;
+    unsigned char* dst = ring + slot * kStageBytes;
     const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
-    for (int i = 0; i < G::DMA_PER_THREAD; ++i) {
+    for (int i = 0; i < kStageBytes / 16 / kThreads; ++i) {
         const int q = i * kThreads + wave * 64;  // first 16-byte chunk of this wave's piece
         __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
     }
 }
 
 __device__ __forceinline__ void wait_dma_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// all but the youngest stage's DMAs complete
-template <int C>
-__device__ __forceinline__ void wait_dma_stage() {
-    if constexpr (Geo<C>::DMA_PER_THREAD == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-}
+// all but the youngest stage's (2 per thread) DMAs complete
+__device__ __forceinline__ void wait_dma_stage() { asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
 
 template <int C, int DT>
 __device__ void heads(const NetView& N, const unsigned char* act, int wave, int lane, int row0, int rows,
                       float* __restrict__ policy, float* __restrict__ value) {
-    constexpr int BOARDS = Geo<C>::BOARDS;
+    using G = Geo<C>;
+    constexpr int BOARDS = G::BOARDS;
     const HeadLayout HL(C, N.hidden);
     const float* hp = N.head;
     const int b = wave % BOARDS;
     const int gr = row0 + b;
     if (wave >= 2 * BOARDS || gr >= rows) return;
-    const int row = b * 64 + lane;
+    const unsigned char* arow = act + (b * G::BROWS + pad_row(lane)) * G::RP;
     if (wave < BOARDS) {
         // policy head: 1x1 conv (C->2) + BN + ReLU, flatten c*64+s, Linear(128->65), softmax
         float h0 = hp[HL.pcb + 0], h1 = hp[HL.pcb + 1];
         for (int c8 = 0; c8 < C / 8; ++c8) {
-            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(act + act_chunk_off<C>(row, c8));
+            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -241,7 +298,7 @@ __device__ void heads(const NetView& N, const unsigned char* act, int wave, int 
         // value head: 1x1 conv (C->1) + BN + ReLU, Linear(64->hidden), ReLU, Linear(hidden->1), tanh
         float v = hp[HL.vcb];
         for (int c8 = 0; c8 < C / 8; ++c8) {
-            const u32x4_t q = *reinterpret_cast<const u32x4_t*>(act + act_chunk_off<C>(row, c8));
+            const u32x4_t q = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
             const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -269,7 +326,17 @@ __device__ void heads(const NetView& N, const unsigned char* act, int wave, int 
     }
 }
 
-template <int C, int DT, int IN>
+template <int C>
+__device__ __forceinline__ void load_bias(float4 (&bv)[4], const NetView& N, int layer, int wn, int lane) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+        bv[n] = *reinterpret_cast<const float4*>(N.bias + (size_t)layer * C + wn * 64 + n * 16 + (lane >> 4) * 4);
+}
+
+// ABL != 0 only in diagnostic ablation builds (OAMD_RESNET_ABLATE, wrong results):
+// bit 0 = no in-loop barrier/DMA wait, 1 = no activation fragment reads,
+// 2 = no weight fragment reads, 3 = no in-loop weight DMA
+template <int C, int DT, int IN, int ABL = 0>
 __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __restrict__ feat_in,
                                                     int fw, int H, int rows,
                                                     float* __restrict__ policy,
@@ -284,20 +351,40 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
     const int lane = tid & 63;
     const int wm = wave / G::WN;  // board of this wave
     const int wn = wave % G::WN;  // 64-channel block of this wave
+    const int kg = lane >> 4;
     const int row0 = blockIdx.x * G::BOARDS;
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
-    const int total = stages_first() + 2 * N.R * stages_tower(C);
+    const int total = (ksteps_first(C) + 2 * N.R * ksteps_tower(C)) / G::KS;
 
     // weight stream starts right away (two stages ahead)
-    issue_stage_dma<C>(wsrc, ring, 0, total, tid);
-    issue_stage_dma<C>(wsrc, ring, 1, total, tid);
+    issue_stage_dma(wsrc, ring, 0, 0, total, tid);
+    issue_stage_dma(wsrc, ring, 1, 1, total, tid);
 
-    // ---------------- input planes -> act channels 0..63 ---------------------
-    if (tid < G::ROWS) {
+    float4 bv[4];  // folded bias of this lane's 16 output channels (current layer)
+    load_bias<C>(bv, N, 0, wn, lane);
+
+    // per-lane bases: fragment reads (row of position tile m + k-group chunk),
+    // epilogue writes (row + k-group's 8-byte half chunk), weight fragments
+    int rd[4], wr[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int rowb = (wm * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) * G::RP;
+        rd[m] = rowb + kgroup_chunk(kg) * 16;
+        wr[m] = rowb + wn * 128 + kg * 8;
+    }
+    const int wl = (wn * 4 * 64 + lane) * 16;
+
+    // ---------------- zero border rows; input planes -> channels 0..31 ------
+    for (int w = tid; w < G::BOARDS * 36 * (C / 8); w += kThreads) {
+        const int c = w % (C / 8), k = (w / (C / 8)) % 36, b = w / (C / 8) / 36;
+        const int r = k < 10 ? k : (k < 20 ? 80 + k : ((k - 20) >> 1) * 10 + 10 + ((k & 1) ? 9 : 0));
+        *reinterpret_cast<u32x4_t*>(act + (b * G::BROWS + r) * G::RP + c * 16) = u32x4_t{0u, 0u, 0u, 0u};
+    }
+    if (tid < G::BOARDS * 64) {
         const int b = tid >> 6, p = tid & 63;
         const int gr = row0 + b;
         const uint32_t one = to_act<DT>(1.0f);
-        uint32_t words[32];  // 64 channels as 16-bit pairs
+        uint32_t words[16];  // 32 channels as 16-bit pairs
         if constexpr (IN == kPacked) {
             uint32_t mask = 0;  // bit c = channel c is 1 (c < 31)
             if (gr < rows) {
@@ -314,146 +401,177 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
                 }
             }
 #pragma unroll
-            for (int w = 0; w < 32; ++w) {
-                const uint32_t lo = (w < 16 && ((mask >> (2 * w)) & 1u)) ? one : 0u;
-                const uint32_t hi = (w < 16 && ((mask >> (2 * w + 1)) & 1u)) ? one : 0u;
+            for (int w = 0; w < 16; ++w) {
+                const uint32_t lo = ((mask >> (2 * w)) & 1u) ? one : 0u;
+                const uint32_t hi = ((mask >> (2 * w + 1)) & 1u) ? one : 0u;
                 words[w] = lo | (hi << 16);
             }
         } else {
             const float* fr = reinterpret_cast<const float*>(feat_in) + (size_t)gr * N.cin * 64;
             const bool ok = gr < rows;
 #pragma unroll
-            for (int w = 0; w < 32; ++w) {
+            for (int w = 0; w < 16; ++w) {
                 const int c0 = 2 * w, c1 = 2 * w + 1;
                 const uint32_t lo = (ok && c0 < N.cin) ? to_act<DT>(fr[c0 * 64 + p]) : 0u;
                 const uint32_t hi = (ok && c1 < N.cin) ? to_act<DT>(fr[c1 * 64 + p]) : 0u;
                 words[w] = lo | (hi << 16);
             }
         }
+        unsigned char* dst = act + (b * G::BROWS + pad_row(p)) * G::RP;
 #pragma unroll
-        for (int ch = 0; ch < 8; ++ch)
-            *reinterpret_cast<u32x4_t*>(act + act_chunk_off<C>(tid, ch)) =
-                u32x4_t{words[4 * ch], words[4 * ch + 1], words[4 * ch + 2], words[4 * ch + 3]};
+        for (int c = 0; c < 4; ++c)
+            *reinterpret_cast<u32x4_t*>(dst + c * 16) =
+                u32x4_t{words[4 * c], words[4 * c + 1], words[4 * c + 2], words[4 * c + 3]};
     }
 
     f32x4_t acc[4][4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) acc[n][m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     u32x2_t skip[4][4];  // residual (block input) of this lane's 64 outputs
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) skip[n][m] = u32x2_t{0u, 0u};
 
     Frags fa, fb;
-    int xrow[4];
-    bool xok[4];
+    int g = 0;     // stage holding the current K-step
+    int slot = 0;  // g % kRing
 
-    // first stage of layer 0: its DMA and the input planes must be visible
+    // stage 0 and the input planes must be visible
     wait_dma_all();
     __syncthreads();
-    tap_rows(0, wm, lane, xrow, xok);
-    load_frags<C>(fa, act, ring, 0, 0, xrow, xok, wn, lane);
+    load_frags(fa, act, ring, kstep_offset<C>(0, true), rd, wl);
 
-    int g = 0;  // global stage index (weight ring position)
     const int nlayers = 1 + 2 * N.R;
-    for (int layer = 0; layer < nlayers; ++layer) {
-        const int S = layer == 0 ? stages_first() : stages_tower(C);
-        const int per_tap = S / 9;  // 64-channel blocks per tap
-        float4 bv[4];               // folded bias of this lane's 16 output channels
+    // one conv layer: KIND 0 = first conv, 1 = a block's first conv (saves the
+    // block input as skip), 2 = a block's second conv (adds skip). Instantiated
+    // per kind so `skip` is live only from conv1's epilogue to conv2's start.
+    auto conv = [&](auto KIND, int layer) {
+        constexpr int kind = decltype(KIND)::value;
+        constexpr bool first = kind == 0;
+        constexpr int nk = first ? ksteps_first(C) : ksteps_tower(C);
+
+        // accumulators start at bias (+ block input for the block's second conv)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-            bv[n] = *reinterpret_cast<const float4*>(N.bias + (size_t)layer * C + wn * 64 + n * 16 +
-                                                     (lane >> 4) * 4);
-        // Stages 0..S-2 share one branch-free body (the waitcnt pass then counts
-        // the outstanding LDS reads exactly and never drains to lgkmcnt(0)).
-        int slot_i = g % kRing;
-        for (int s = 0; s + 1 < S; ++s, ++g) {
-            const int cb64 = s % per_tap;
-            const unsigned char* slot = ring + slot_i * G::STAGE_BYTES;
-            // second K-step of this stage; its reads overlap the first MFMAs
-            load_frags<C>(fb, act, slot, 1, cb64, xrow, xok, wn, lane);
-            mfma_frags<DT>(acc, fa);
-            // stage g+1 landed (issued one stage ago); stage g-1 drained by all waves
-            wait_dma_all();
-            __builtin_amdgcn_s_barrier();
-            issue_stage_dma<C>(wsrc, ring, g + 2, total, tid);
-            slot_i = slot_i == kRing - 1 ? 0 : slot_i + 1;
-            tap_rows((s + 1) / per_tap, wm, lane, xrow, xok);
-            load_frags<C>(fa, act, ring + slot_i * G::STAGE_BYTES, 0, (s + 1) % per_tap, xrow, xok, wn, lane);
-            mfma_frags<DT>(acc, fb);
-        }
-        {  // last stage of the layer
-            load_frags<C>(fb, act, ring + slot_i * G::STAGE_BYTES, 1, (S - 1) % per_tap, xrow, xok, wn, lane);
-            mfma_frags<DT>(acc, fa);
-            mfma_frags<DT>(acc, fb);
-            ++g;
-        }
-
-        // ---------------- epilogue: bias (+ skip) + ReLU, in place ------------
-        // g is now the first stage of the next layer (its DMA is in flight)
-        __syncthreads();  // every wave is done reading this layer's input and stage g-1
-        issue_stage_dma<C>(wsrc, ring, g + 1, total, tid);  // hidden behind the epilogue
-        const bool is_conv1 = layer > 0 && ((layer - 1) & 1) == 0;
-        const bool is_conv2 = layer > 0 && ((layer - 1) & 1) == 1;
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const int ch = wn * 64 + n * 16 + (lane >> 4) * 4;
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                const int row = wm * 64 + m * 16 + (lane & 15);
-                const int off = act_chunk_off<C>(row, ch >> 3) + (ch & 7) * 2;
-                u32x2_t* p = reinterpret_cast<u32x2_t*>(act + off);
-                float v0 = acc[n][m][0] + bv[n].x, v1 = acc[n][m][1] + bv[n].y;
-                float v2 = acc[n][m][2] + bv[n].z, v3 = acc[n][m][3] + bv[n].w;
-                if (is_conv1) skip[n][m] = *p;  // block input, needed by conv2's epilogue
-                if (is_conv2) {
+                f32x4_t a = f32x4_t{bv[n].x, bv[n].y, bv[n].z, bv[n].w};
+                if constexpr (kind == 2) {
                     const u32x2_t r = skip[n][m];
-                    v0 += from_act<DT>(r.x & 0xffffu);
-                    v1 += from_act<DT>(r.x >> 16);
-                    v2 += from_act<DT>(r.y & 0xffffu);
-                    v3 += from_act<DT>(r.y >> 16);
+                    a[0] += from_act<DT>(r.x & 0xffffu);
+                    a[1] += from_act<DT>(r.x >> 16);
+                    a[2] += from_act<DT>(r.y & 0xffffu);
+                    a[3] += from_act<DT>(r.y >> 16);
                 }
-                v0 = fmaxf(v0, 0.f);
-                v1 = fmaxf(v1, 0.f);
-                v2 = fmaxf(v2, 0.f);
-                v3 = fmaxf(v3, 0.f);
-                *p = u32x2_t{to_act<DT>(v0) | (to_act<DT>(v1) << 16), to_act<DT>(v2) | (to_act<DT>(v3) << 16)};
-                acc[n][m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                acc[n][m] = a;
             }
+
+        // step: load K-step i1's fragments into nxt, then MFMAs on cur (K-step i1-1).
+        // NEW: i1 opens a new stage -> DMA wait + barrier, ring advances.
+        auto step = [&](auto NEW, const Frags& cur, Frags& nxt, int i1) {
+            if constexpr (decltype(NEW)::value) {
+                // stage g+1 landed (issued one stage ago); stage g-1 drained by all waves
+                if constexpr (!(ABL & 1)) {
+                    wait_dma_all();
+                    __builtin_amdgcn_s_barrier();
+                }
+                const int s2 = slot == 0 ? 2 : slot - 1;  // (g + 2) % kRing
+                if constexpr (!(ABL & 8)) issue_stage_dma(wsrc, ring, g + 2, s2, total, tid);
+                ++g;
+                slot = slot == kRing - 1 ? 0 : slot + 1;
+            }
+            constexpr int kis = decltype(NEW)::value ? 0 : 1;  // K-step within its stage
+            load_frags<ABL>(nxt, act, ring + slot * kStageBytes + kis * G::KSTEP_BYTES,
+                            kstep_offset<C>(i1, first), rd, wl);
+            mfma_frags<DT>(acc, cur);
+        };
+        using NewOdd = std::integral_constant<bool, G::KS == 1>;  // K-step i1 odd
+        using NewEven = std::integral_constant<bool, true>;       // K-step i1 even
+        int i = 0;
+        for (; i + 2 < nk; i += 2) {
+            step(NewOdd{}, fa, fb, i + 1);
+            step(NewEven{}, fb, fa, i + 2);
         }
-        if (layer + 1 < nlayers) {
-            wait_dma_stage<C>();  // stage g has landed (stage g+1 may still fly)
-            __syncthreads();      // ... and this layer's output is complete
-            tap_rows(0, wm, lane, xrow, xok);
-            load_frags<C>(fa, act, ring + (g % kRing) * G::STAGE_BYTES, 0, 0, xrow, xok, wn, lane);
+        if constexpr (nk % 2 == 0) {
+            step(NewOdd{}, fa, fb, nk - 1);
+            mfma_frags<DT>(acc, fb);
+        } else {
+            mfma_frags<DT>(acc, fa);
         }
+
+        // ---------------- epilogue: ReLU, in place --------------------------
+        // stage g+1 (next layer's first) is in flight; the next layer's bias is
+        // loaded before the next DMA so the DMA wait below does not cover it
+        const bool more = layer + 1 < nlayers;
+        if (more) load_bias<C>(bv, N, layer + 1, wn, lane);
+        __syncthreads();  // every wave is done reading this layer's input and stage g
+        issue_stage_dma(wsrc, ring, g + 2, slot == 0 ? 2 : slot - 1, total, tid);  // behind the epilogue
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                u32x2_t* p = reinterpret_cast<u32x2_t*>(act + wr[m] + n * 32);
+                if constexpr (kind == 1) skip[n][m] = *p;  // block input, needed by conv2
+                const f32x4_t a = acc[n][m];
+                *p = u32x2_t{pack_relu<DT>(a[0], a[1]), pack_relu<DT>(a[2], a[3])};
+            }
+        ++g;
+        slot = slot == kRing - 1 ? 0 : slot + 1;
+        if (more) {
+            wait_dma_stage();  // stage g has landed (stage g+1 may still fly)
+            __syncthreads();   // ... and this layer's output is complete
+            load_frags(fa, act, ring + slot * kStageBytes, kstep_offset<C>(0, false), rd, wl);
+        }
+    };
+    conv(std::integral_constant<int, 0>{}, 0);
+    for (int blk = 0; blk < N.R; ++blk) {
+        conv(std::integral_constant<int, 1>{}, 1 + 2 * blk);
+        conv(std::integral_constant<int, 2>{}, 2 + 2 * blk);
     }
     __syncthreads();
     heads<C, DT>(N, act, wave, lane, row0, rows, policy, value);
 }
 
-template <int C, int DT, int IN>
+template <int C, int DT, int IN, int ABL = 0>
 static void launch_t(const NetView& N, const void* feat, int fw, int H, int rows, float* pol,
                      float* val, hipStream_t s) {
     using G = Geo<C>;
     const unsigned grid = (unsigned)((rows + G::BOARDS - 1) / G::BOARDS);
     static bool configured = false;
     if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_resnet<C, DT, IN>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_resnet<C, DT, IN, ABL>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         configured = true;
     }
-    hipLaunchKernelGGL((k_resnet<C, DT, IN>), dim3(grid), dim3(kThreads), G::LDS, s, N, feat, fw, H,
+    hipLaunchKernelGGL((k_resnet<C, DT, IN, ABL>), dim3(grid), dim3(kThreads), G::LDS, s, N, feat, fw, H,
                        rows, pol, val);
 }
+
+#ifdef OAMD_ABLATION
+static int ablation() {
+    static int v = [] {
+        const char* e = getenv("OAMD_RESNET_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+#endif
 
 template <int IN>
 static void dispatch(const NetView& N, const void* feat, int fw, int H, int rows, float* pol,
                      float* val, hipStream_t s) {
     if (rows <= 0) return;
+#ifdef OAMD_ABLATION
+    if constexpr (IN == kF32) {
+        if (N.C == 128 && N.dtype == OAMD_BF16 && ablation()) {
+            switch (ablation()) {
+                case 1: return launch_t<128, OAMD_BF16, IN, 1>(N, feat, fw, H, rows, pol, val, s);
+                case 2: return launch_t<128, OAMD_BF16, IN, 2>(N, feat, fw, H, rows, pol, val, s);
+                case 4: return launch_t<128, OAMD_BF16, IN, 4>(N, feat, fw, H, rows, pol, val, s);
+                case 6: return launch_t<128, OAMD_BF16, IN, 6>(N, feat, fw, H, rows, pol, val, s);
+                case 8: return launch_t<128, OAMD_BF16, IN, 8>(N, feat, fw, H, rows, pol, val, s);
+                case 9: return launch_t<128, OAMD_BF16, IN, 9>(N, feat, fw, H, rows, pol, val, s);
+                case 15: return launch_t<128, OAMD_BF16, IN, 15>(N, feat, fw, H, rows, pol, val, s);
+                default: break;
+            }
+        }
+    }
+#endif
     if (N.C == 128) {
         if (N.dtype == OAMD_FP16) launch_t<128, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
         else launch_t<128, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);

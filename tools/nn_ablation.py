@@ -1,0 +1,34 @@
+"""Diagnostic: time the fused ResNet kernel (or an ablation variant selected by
+OAMD_RESNET_ABLATE, extension built with OAMD_EXTRA_FLAGS=-DOAMD_ABLATION).
+Ablation variants produce wrong outputs; only their timings matter.
+Prints one line: variant, ms per launch (median of 5 x 10 launches), TFLOP/s."""
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "othello-alphazero_amd"))
+import torch  # noqa: E402
+
+import othello_mcts as om  # noqa: E402
+from othello_mcts.synthetic import alphazero_state_dict  # noqa: E402
+
+rows = int(os.environ.get("ROWS", "8192"))
+v = os.environ.get("OAMD_RESNET_ABLATE", "0")
+net = om.NativeNet(alphazero_state_dict(1, 17, 128, 9, 128), device=0)
+x = (torch.rand((rows, 17, 8, 8), device="cuda") < 0.3).float()
+for _ in range(3):
+    net(x)
+torch.cuda.synchronize()
+ms = []
+for _ in range(5):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(10):
+        net(x)
+    b.record()
+    torch.cuda.synchronize()
+    ms.append(a.elapsed_time(b) / 10)
+ms.sort()
+t = ms[len(ms) // 2]
+print(f"variant {v}: {t:.3f} ms/launch  {342327808.0 * rows / t / 1e9:.1f} TFLOP/s  (rows={rows})", flush=True)
