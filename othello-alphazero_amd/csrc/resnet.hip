@@ -50,8 +50,30 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int kThreads = 512;
-constexpr int kRing = 3;         // weight ring slots
-constexpr int kStageBytes = 16384;
+constexpr int kLdsBytes = 160 * 1024;
+// Weight stage = 16 KiB (2 K-steps at C=128, 1 at C=256) in a 3-slot ring.
+// Compile-time schedule knobs, A/B-measured on MI355X with tools/ab.sh (same box,
+// k_resnet 8192 rows, C=128): 16 KiB stages beat 8 KiB stages in a 6-slot ring
+// (4 stages in flight) by 3 %; the per-step fence (OAMD_FENCE) gains 2 %;
+// forcing reads before MFMAs (OAMD_READS_FIRST), placing the DMA between MFMAs
+// (OAMD_DMA_LATE) and s_setprio around MFMA runs (OAMD_PRIO) each lose 1-4 %.
+#ifndef OAMD_STAGE128
+#define OAMD_STAGE128 16384
+#endif
+#ifndef OAMD_PRIO
+#define OAMD_PRIO 0
+#endif
+#ifndef OAMD_READS_FIRST
+#define OAMD_READS_FIRST 0
+#endif
+#ifndef OAMD_FENCE
+#define OAMD_FENCE 1
+#endif
+#ifndef OAMD_DMA_LATE
+#define OAMD_DMA_LATE 0
+#endif
+template <int C>
+__host__ __device__ constexpr int stage_bytes() { return C == 128 ? OAMD_STAGE128 : 16384; }
 
 // Head parameter buffer layout (fp32), filled by oamd_net_load_state (capi.hip).
 struct HeadLayout {
@@ -74,7 +96,9 @@ struct HeadLayout {
 size_t resnet_head_floats(int C, int hidden) { return (size_t)HeadLayout(C, hidden).total; }
 
 // ---- K-step schedule (shared with the host packer) --------------------------
-__host__ __device__ constexpr int ksteps_per_stage(int C) { return kStageBytes / (32 * C * 2); }
+__host__ __device__ constexpr int ksteps_per_stage(int C) {
+    return (C == 128 ? stage_bytes<128>() : stage_bytes<256>()) / (32 * C * 2);
+}
 __host__ __device__ constexpr int ksteps_first(int C) {
     return (9 + ksteps_per_stage(C) - 1) / ksteps_per_stage(C) * ksteps_per_stage(C);
 }
@@ -133,10 +157,15 @@ struct Geo {
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
     static constexpr int KS = ksteps_per_stage(C);
     static constexpr int KSTEP_BYTES = 32 * C * 2;
-    static constexpr int DMA_PER_THREAD = kStageBytes / 16 / kThreads;
-    static constexpr int LDS = ACT_BYTES + kRing * kStageBytes;
-    static_assert(LDS <= 160 * 1024, "LDS budget");
-    static_assert(DMA_PER_THREAD == 2, "wait_dma_stage assumes 2 DMAs per thread per stage");
+    static constexpr int STAGE = stage_bytes<C>();
+    static constexpr int DPT = STAGE / 16 / kThreads;        // DMAs per thread per stage
+    static constexpr int RING = (kLdsBytes - ACT_BYTES) / STAGE;  // weight ring slots
+    static constexpr int LDS = ACT_BYTES + RING * STAGE;
+    // The slot of stage s + RING - 2 is issued at the barrier that opens stage s,
+    // so RING - 2 stages are in flight while one is read.
+    static constexpr int VM_OPEN = (RING - 3) * DPT;   // vmcnt at a stage-opening barrier
+    static constexpr int VM_LAYER = (RING - 2) * DPT;  // vmcnt after an epilogue's extra issue
+    static_assert(RING >= 3 && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
 };
 
 template <int DT>
@@ -223,28 +252,46 @@ __device__ __forceinline__ void load_frags(Frags& f, const unsigned char* act, c
 
 template <int DT>
 __device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[4][4], const Frags& f) {
+    if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
+    if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
+// Stages past the last one re-read the last stage into a slot nobody reads any
+// more: the issue stays branch-free and the vmcnt bookkeeping uniform.
+template <int C>
 __device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsigned char* ring, int g, int slot,
                                                 int total, int tid) {
-    if (g >= total) return;
-    const unsigned char* src = wsrc + (size_t)g * kStageBytes;
-    unsigned char* dst = ring + slot * kStageBytes;
+    using G = Geo<C>;
+    const unsigned char* src = wsrc + (size_t)(g < total ? g : total - 1) * G::STAGE;
+    unsigned char* dst = ring + slot * G::STAGE;
     const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
-    for (int i = 0; i < kStageBytes / 16 / kThreads; ++i) {
+    for (int i = 0; i < G::DPT; ++i) {
         const int q = i * kThreads + wave * 64;  // first 16-byte chunk of this wave's piece
         __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
     }
 }
 
-__device__ __forceinline__ void wait_dma_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// all but the youngest stage's (2 per thread) DMAs complete
-__device__ __forceinline__ void wait_dma_stage() { asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
+// s_waitcnt vmcnt(N): all but this wave's N youngest LDS-DMA / global ops done
+// (gfx9 encoding: vmcnt[3:0], expcnt[6:4] = 7, lgkmcnt[11:8] = 15: no wait on those)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 16, "vmcnt");
+    __builtin_amdgcn_s_waitcnt(N | 0x0F70);
+    asm volatile("" ::: "memory");
+}
+
+// Workgroup barrier that keeps LDS-DMA in flight: __syncthreads()' fence would
+// add vmcnt(0). This wave's LDS accesses complete first (lgkmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 
 template <int C, int DT>
 __device__ void heads(const NetView& N, const unsigned char* act, int wave, int lane, int row0, int rows,
@@ -356,9 +403,9 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
     const int total = (ksteps_first(C) + 2 * N.R * ksteps_tower(C)) / G::KS;
 
-    // weight stream starts right away (two stages ahead)
-    issue_stage_dma(wsrc, ring, 0, 0, total, tid);
-    issue_stage_dma(wsrc, ring, 1, 1, total, tid);
+    // weight stream starts right away: stages 0 .. RING-2
+#pragma unroll
+    for (int s = 0; s + 1 < G::RING; ++s) issue_stage_dma<C>(wsrc, ring, s, s, total, tid);
 
     float4 bv[4];  // folded bias of this lane's 16 output channels (current layer)
     load_bias<C>(bv, N, 0, wn, lane);
@@ -429,11 +476,11 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
 
     Frags fa, fb;
     int g = 0;     // stage holding the current K-step
-    int slot = 0;  // g % kRing
+    int slot = 0;  // g % RING
 
-    // stage 0 and the input planes must be visible
-    wait_dma_all();
-    __syncthreads();
+    // stage 0 and the input planes must be visible (bias loads are older than the DMAs)
+    wait_vm<G::VM_LAYER>();
+    lds_barrier();
     load_frags(fa, act, ring, kstep_offset<C>(0, true), rd, wl);
 
     const int nlayers = 1 + 2 * N.R;
@@ -464,21 +511,48 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
         // step: load K-step i1's fragments into nxt, then MFMAs on cur (K-step i1-1).
         // NEW: i1 opens a new stage -> DMA wait + barrier, ring advances.
         auto step = [&](auto NEW, const Frags& cur, Frags& nxt, int i1) {
-            if constexpr (decltype(NEW)::value) {
-                // stage g+1 landed (issued one stage ago); stage g-1 drained by all waves
+            constexpr bool open = decltype(NEW)::value;
+#if OAMD_FENCE
+            // keep each step's MFMAs (on cur) with the fragment reads they hide:
+            // without this fence the scheduler may hoist the next step's MFMAs over
+            // the barrier right behind their reads and drain lgkmcnt each step
+            __builtin_amdgcn_sched_barrier(0);
+            // cur's reads (issued a step ago, 16 MFMAs of cover) are done: retire
+            // them before issuing nxt's, or 16 outstanding reads overflow the
+            // 4-bit lgkmcnt and the compiler drains nxt's reads too
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+#endif
+            int sp = 0;
+            if constexpr (open) {
+                // open stage g+1: it has landed (this wave's DMAs, then everyone's
+                // via the barrier) and stage g-1's slot is drained by all waves
                 if constexpr (!(ABL & 1)) {
-                    wait_dma_all();
+                    wait_vm<G::VM_OPEN>();
                     __builtin_amdgcn_s_barrier();
                 }
-                const int s2 = slot == 0 ? 2 : slot - 1;  // (g + 2) % kRing
-                if constexpr (!(ABL & 8)) issue_stage_dma(wsrc, ring, g + 2, s2, total, tid);
+                sp = slot == 0 ? G::RING - 1 : slot - 1;  // (g + RING - 1) % RING
+                if constexpr (!(ABL & 8) && !OAMD_DMA_LATE)
+                    issue_stage_dma<C>(wsrc, ring, g + G::RING - 1, sp, total, tid);
                 ++g;
-                slot = slot == kRing - 1 ? 0 : slot + 1;
+                slot = slot == G::RING - 1 ? 0 : slot + 1;
             }
-            constexpr int kis = decltype(NEW)::value ? 0 : 1;  // K-step within its stage
-            load_frags<ABL>(nxt, act, ring + slot * kStageBytes + kis * G::KSTEP_BYTES,
+            constexpr int kis = open ? 0 : 1;  // K-step within its stage
+            load_frags<ABL>(nxt, act, ring + slot * G::STAGE + kis * G::KSTEP_BYTES,
                             kstep_offset<C>(i1, first), rd, wl);
+            if constexpr (open && !(ABL & 8) && OAMD_DMA_LATE)
+                issue_stage_dma<C>(wsrc, ring, g + G::RING - 2, sp, total, tid);
             mfma_frags<DT>(acc, cur);
+#if OAMD_READS_FIRST
+            // issue the 8 fragment reads first, the stage DMA a few MFMAs later
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+            if constexpr (open && OAMD_DMA_LATE) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+            } else {
+                __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+            }
+#endif
         };
         using NewOdd = std::integral_constant<bool, G::KS == 1>;  // K-step i1 odd
         using NewEven = std::integral_constant<bool, true>;       // K-step i1 even
@@ -495,12 +569,12 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
         }
 
         // ---------------- epilogue: ReLU, in place --------------------------
-        // stage g+1 (next layer's first) is in flight; the next layer's bias is
-        // loaded before the next DMA so the DMA wait below does not cover it
+        // stages g+1 .. (next layer's) are in flight; the next layer's bias is
+        // loaded before the next DMA so the counted wait below covers it
         const bool more = layer + 1 < nlayers;
         if (more) load_bias<C>(bv, N, layer + 1, wn, lane);
-        __syncthreads();  // every wave is done reading this layer's input and stage g
-        issue_stage_dma(wsrc, ring, g + 2, slot == 0 ? 2 : slot - 1, total, tid);  // behind the epilogue
+        lds_barrier();  // every wave is done reading this layer's input and stage g
+        issue_stage_dma<C>(wsrc, ring, g + G::RING - 1, slot == 0 ? G::RING - 1 : slot - 1, total, tid);
 #pragma unroll
         for (int n = 0; n < 4; ++n)
 #pragma unroll
@@ -511,11 +585,11 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
                 *p = u32x2_t{pack_relu<DT>(a[0], a[1]), pack_relu<DT>(a[2], a[3])};
             }
         ++g;
-        slot = slot == kRing - 1 ? 0 : slot + 1;
+        slot = slot == G::RING - 1 ? 0 : slot + 1;
         if (more) {
-            wait_dma_stage();  // stage g has landed (stage g+1 may still fly)
-            __syncthreads();   // ... and this layer's output is complete
-            load_frags(fa, act, ring + slot * kStageBytes, kstep_offset<C>(0, false), rd, wl);
+            wait_vm<G::VM_LAYER>();  // stage g has landed (later stages may still fly)
+            lds_barrier();           // ... and this layer's output is complete
+            load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false), rd, wl);
         }
     };
     conv(std::integral_constant<int, 0>{}, 0);
