@@ -83,6 +83,42 @@ def cpu_baseline(seconds: float, history: int, C: int, R: int, hidden: int) -> d
                       f"eps=0.25), {C}x{R + 1}b fp32 torch-CPU, {dt:.1f} s"}
 
 
+# ---- multi-GPU plumbing (one process per GPU; games shard, no data-path
+# collective). Kept device-agnostic so tests/test_dist_cpu.py runs it with gloo.
+
+def dist_env() -> tuple[int, int, int]:
+    """(world, rank, local_rank) from the torchrun environment (1, 0, 0 if unset)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard_seeds(seed: int, rank: int) -> tuple[int, int]:
+    """Per-rank (engine RNG key, opening seed): every rank plays its own games."""
+    return seed + 7919 * rank, seed + rank
+
+
+def timed_max(world: int, run, sync, device: str) -> float:
+    """Run `run()` bracketed by barrier + device sync on both sides; return the
+    MAX wall time over ranks (the whole job's time)."""
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    run()
+    sync()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate_rate(world: int, games: int, sims_per_search: int, steps: int, dt_max: float) -> float:
+    """Whole-job simulations/s: the units all ranks processed / the max time."""
+    return world * games * sims_per_search * steps / dt_max
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -101,9 +137,7 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=2025)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = dist_env()
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -114,9 +148,10 @@ def main() -> None:
     R = args.blocks - 1
     sd = alphazero_state_dict(args.seed, 1 + 2 * args.history, args.channels, R, args.hidden)
     net = om.NativeNet(sd, device=local, dtype=args.dtype)
+    engine_seed, opening_seed = shard_seeds(args.seed, rank)
     b = om.BatchedMCTS(args.games, history_size=args.history, num_simulations=args.sims,
-                       num_threads=args.threads, batch_size=args.batch, seed=args.seed + 7919 * rank)
-    b.random_openings(8, seed=args.seed + rank)
+                       num_threads=args.threads, batch_size=args.batch, seed=engine_seed)
+    b.random_openings(8, seed=opening_seed)
     L = args.threads * args.batch
     sims_per_search = L * ((args.sims + L - 1) // L)
 
@@ -129,26 +164,14 @@ def main() -> None:
     torch.cuda.synchronize()
     b.engine.enable_timing(True)
     ms0, launches0, rows0 = b.engine.nn_timing()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    evals = 0
-    for _ in range(args.steps):
-        b.search(net)  # counters: evaluated (non-terminal) leaves
-        b.selfplay_move(temperature_moves=12, opening_moves=8, emit_targets=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+
+    def run():
+        for _ in range(args.steps):
+            step()
+
+    dt_max = timed_max(world, run, torch.cuda.synchronize, "cuda")
     ms1, launches1, rows1 = b.engine.nn_timing()
-    # evaluated rows: re-run counters cheaply from the search return values
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt_max = float(t.item())
-    total_sims = world * args.games * sims_per_search * args.steps
-    value = total_sims / dt_max
+    value = aggregate_rate(world, args.games, sims_per_search, args.steps, dt_max)
 
     nn_ms = ms1 - ms0
     nn_launches = launches1 - launches0
@@ -158,11 +181,17 @@ def main() -> None:
     rows_per_launch = nn_rows / max(1, nn_launches)
     achieved = flops * rows_per_launch / (avg_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
+    workload = (f"{args.games} concurrent self-play games per GPU, {args.sims} sims/move, "
+                f"{args.channels}x{args.blocks}b ResNet {args.dtype}, history {args.history}, "
+                f"{args.threads} threads x {args.batch} leaves per step (BASELINE configs[1])")
+    # HBM bytes per launch from the committed PMC summary of this same workload
     traffic = None
     tfile = ROOT / "profiles" / "traffic_resnet.json"
     if tfile.exists():
         try:
-            traffic = json.loads(tfile.read_text()).get("bytes_per_launch")
+            tj = json.loads(tfile.read_text())
+            if tj.get("workload") == workload and tj.get("rows_per_launch") == int(rows_per_launch):
+                traffic = tj.get("bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
 
@@ -180,9 +209,7 @@ def main() -> None:
         "dtype": args.dtype,
         "data": "synthetic: seeded random-init 128x10b AlphaZeroNet weights, random openings (0-8 plies)",
         "config": {
-            "workload": f"{args.games} concurrent self-play games per GPU, {args.sims} sims/move, "
-                        f"{args.channels}x{args.blocks}b ResNet {args.dtype}, history {args.history}, "
-                        f"{args.threads} threads x {args.batch} leaves per step (BASELINE configs[1])",
+            "workload": workload,
             "games_per_gpu": args.games,
             "sims_per_move": args.sims,
             "leaves_per_step": L,

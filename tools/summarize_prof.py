@@ -39,6 +39,13 @@ def main(tag: str) -> None:
         for c, v in cs.items():
             k[c + "_per_launch"] = sum(v) / len(v)
     res = kern.get("k_resnet", {})
+    # the bench line of the traced run names the workload the counters belong to
+    bench_line = None
+    log = PROF / "trace.log"
+    if log.exists():
+        for ln in log.read_text().splitlines():
+            if ln.startswith("{") and '"metric"' in ln:
+                bench_line = json.loads(ln)
     if "FETCH_SIZE_per_launch" in res and "WRITE_SIZE_per_launch" in res:
         fetch = 2.0 * res["FETCH_SIZE_per_launch"] * 1024  # gfx950 FETCH_SIZE correction
         write = res["WRITE_SIZE_per_launch"] * 1024
@@ -46,6 +53,8 @@ def main(tag: str) -> None:
         (OUT / "traffic_resnet.json").write_text(json.dumps({
             "tag": tag, "bytes_per_launch": round(fetch + write),
             "fetch_bytes_corrected": round(fetch), "write_bytes": round(write),
+            "workload": bench_line["config"]["workload"] if bench_line else None,
+            "rows_per_launch": bench_line["roofline"]["rows_per_launch"] if bench_line else None,
             "note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> B), rocprofv3 --pmc, separate passes"}, indent=1))
     if "SQ_VALU_MFMA_BUSY_CYCLES_per_launch" in res and "GRBM_GUI_ACTIVE_per_launch" in res:
         # SQ_VALU_MFMA_BUSY_CYCLES sums MFMA-busy cycles over all SIMDs (1024 on MI355X);
