@@ -72,6 +72,9 @@ constexpr int kLdsBytes = 160 * 1024;
 #ifndef OAMD_DMA_LATE
 #define OAMD_DMA_LATE 0
 #endif
+#ifndef OAMD_STAGGER
+#define OAMD_STAGGER 0
+#endif
 template <int C>
 __host__ __device__ constexpr int stage_bytes() { return C == 128 ? OAMD_STAGE128 : 16384; }
 
@@ -248,6 +251,15 @@ __device__ __forceinline__ void load_frags(Frags& f, const unsigned char* act, c
     const unsigned char* ap = act + aoff;
 #pragma unroll
     for (int m = 0; m < 4; ++m) f.x[m] = *reinterpret_cast<const u32x4_t*>(ap + rd[m]);
+}
+
+// half h of a K-step's MFMAs: output channel tiles n = 2h, 2h+1
+template <int DT>
+__device__ __forceinline__ void mfma_half(f32x4_t (&acc)[4][4], const Frags& f, int h) {
+#pragma unroll
+    for (int n = 2 * h; n < 2 * h + 2; ++n)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
 }
 
 template <int DT>
@@ -510,18 +522,26 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
 
         // step: load K-step i1's fragments into nxt, then MFMAs on cur (K-step i1-1).
         // NEW: i1 opens a new stage -> DMA wait + barrier, ring advances.
-        auto step = [&](auto NEW, const Frags& cur, Frags& nxt, int i1) {
+        // GB = waves 4-7 (the SIMD partners of waves 0-3) with OAMD_STAGGER: half
+        // of cur's MFMAs go before the barrier, so while waves 0-3 issue the
+        // post-barrier DMA and reads, their partners keep the MFMA pipe busy
+        auto step = [&](auto NEW, auto GB, const Frags& cur, Frags& nxt, int i1) {
             constexpr bool open = decltype(NEW)::value;
+            constexpr bool gb = decltype(GB)::value;
 #if OAMD_FENCE
             // keep each step's MFMAs (on cur) with the fragment reads they hide:
             // without this fence the scheduler may hoist the next step's MFMAs over
             // the barrier right behind their reads and drain lgkmcnt each step
             __builtin_amdgcn_sched_barrier(0);
-            // cur's reads (issued a step ago, 16 MFMAs of cover) are done: retire
-            // them before issuing nxt's, or 16 outstanding reads overflow the
-            // 4-bit lgkmcnt and the compiler drains nxt's reads too
+            // cur's reads (issued a step ago) are done: retire them before
+            // issuing nxt's, or 16 outstanding reads overflow the 4-bit lgkmcnt
+            // and the compiler drains nxt's reads too
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
 #endif
+            if constexpr (gb) {
+                mfma_half<DT>(acc, cur, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             int sp = 0;
             if constexpr (open) {
                 // open stage g+1: it has landed (this wave's DMAs, then everyone's
@@ -541,31 +561,42 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
                             kstep_offset<C>(i1, first), rd, wl);
             if constexpr (open && !(ABL & 8) && OAMD_DMA_LATE)
                 issue_stage_dma<C>(wsrc, ring, g + G::RING - 2, sp, total, tid);
-            mfma_frags<DT>(acc, cur);
+            if constexpr (gb) {
+                mfma_half<DT>(acc, cur, 1);
+            } else {
+                mfma_frags<DT>(acc, cur);
+            }
 #if OAMD_READS_FIRST
             // issue the 8 fragment reads first, the stage DMA a few MFMAs later
             __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
             if constexpr (open && OAMD_DMA_LATE) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
                 __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, gb ? 4 : 12, 0);
             } else {
-                __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, gb ? 8 : 16, 0);
             }
 #endif
         };
         using NewOdd = std::integral_constant<bool, G::KS == 1>;  // K-step i1 odd
         using NewEven = std::integral_constant<bool, true>;       // K-step i1 even
-        int i = 0;
-        for (; i + 2 < nk; i += 2) {
-            step(NewOdd{}, fa, fb, i + 1);
-            step(NewEven{}, fb, fa, i + 2);
-        }
-        if constexpr (nk % 2 == 0) {
-            step(NewOdd{}, fa, fb, nk - 1);
-            mfma_frags<DT>(acc, fb);
+        auto kloop = [&](auto GB) {
+            int i = 0;
+            for (; i + 2 < nk; i += 2) {
+                step(NewOdd{}, GB, fa, fb, i + 1);
+                step(NewEven{}, GB, fb, fa, i + 2);
+            }
+            if constexpr (nk % 2 == 0) {
+                step(NewOdd{}, GB, fa, fb, nk - 1);
+                mfma_frags<DT>(acc, fb);
+            } else {
+                mfma_frags<DT>(acc, fa);
+            }
+        };
+        if (OAMD_STAGGER && wave >= 4) {
+            kloop(std::true_type{});
         } else {
-            mfma_frags<DT>(acc, fa);
+            kloop(std::false_type{});
         }
 
         // ---------------- epilogue: ReLU, in place --------------------------

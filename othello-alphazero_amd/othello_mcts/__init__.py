@@ -3,8 +3,10 @@
 Same import surface as cpp/src/othello_mcts/__init__.py:1-6 (``MCTS``,
 ``Position``, ``get_flips``, ``get_legal_moves``), backed by hand-written HIP
 kernels for gfx950 behind the C ABI in include/othello_mcts_amd.h. Additive
-API: ``BatchedMCTS`` (G games per GPU, on-device self-play driver) and
-``NativeNet`` (fused bf16/fp16 AlphaZeroNet forward).
+API: ``BatchedMCTS`` (G games per GPU, on-device self-play driver),
+``NativeNet`` (fused bf16/fp16 AlphaZeroNet forward, also from a reference
+checkpoint directory via ``load_checkpoint``) and ``SelfPlayCollector`` /
+``self_play`` (training samples in the reference's ``_self_play`` format).
 
 There is no CPU fallback: importing works anywhere the extension was built,
 but creating a search object needs a ROCm GPU and raises otherwise.
@@ -24,7 +26,8 @@ from ._othello_mcts_impl import (  # noqa: F401
     get_legal_moves,
 )
 from .batched import BatchedMCTS  # noqa: E402,F401
-from .native import NativeNet  # noqa: E402,F401
+from .native import NativeNet, load_checkpoint  # noqa: E402,F401
+from .selfplay import SelfPlayCollector, self_play  # noqa: E402,F401
 
 __all__ = [
     "MCTS",
@@ -34,4 +37,7 @@ __all__ = [
     "BatchedMCTS",
     "NativeNet",
     "SearchConfig",
+    "SelfPlayCollector",
+    "load_checkpoint",
+    "self_play",
 ]

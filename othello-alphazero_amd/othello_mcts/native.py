@@ -19,8 +19,10 @@ to always call the Python module instead (the reference's exact numerics).
 
 from __future__ import annotations
 
+import json
 import os
 import weakref
+from pathlib import Path
 
 import numpy as np
 import torch
@@ -40,8 +42,38 @@ def _to_numpy_state(sd) -> dict[str, np.ndarray]:
     return out
 
 
+def load_checkpoint(checkpoint_dir) -> tuple[dict, dict]:
+    """Read a reference checkpoint directory: ``config.json`` + ``neural_net.pth``
+    as written by train.py:299-313 and read by player.py:195-228 (same
+    in_channels validation and messages). The state_dict is loaded with
+    ``weights_only=True`` on the CPU. Returns (config, state_dict); the
+    ``config["neural_net"]`` entries must agree with the state_dict's shapes."""
+    checkpoint_dir = Path(checkpoint_dir)
+    with (checkpoint_dir / "config.json").open(encoding="utf-8") as f:
+        config = json.load(f)
+    in_channels = config["neural_net"]["in_channels"]
+    if in_channels % 2 != 1:
+        raise ValueError(f"Expected in_channels to be odd, but got {in_channels}.")
+    history_size = (in_channels - 1) // 2
+    if history_size < 1:
+        raise ValueError(f"Expected history_size to be positive, but got {history_size}.")
+    sd = torch.load(checkpoint_dir / "neural_net.pth", map_location="cpu", weights_only=True)
+    got = net_config_from_state_dict(sd)
+    for k, v in config["neural_net"].items():
+        if k in got and got[k] != v:
+            raise ValueError(f"config.json neural_net.{k} = {v} but neural_net.pth has {got[k]}")
+    return config, sd
+
+
 class NativeNet:
     """Fused-kernel AlphaZeroNet on one GPU (eval mode only)."""
+
+    @classmethod
+    def from_checkpoint(cls, checkpoint_dir, device: int | str | torch.device | None = None,
+                        dtype: str = "bf16") -> "NativeNet":
+        """NativeNet from a reference checkpoint directory (load_checkpoint)."""
+        _, sd = load_checkpoint(checkpoint_dir)
+        return cls(sd, device=device, dtype=dtype)
 
     def __init__(self, net_or_state_dict, device: int | str | torch.device | None = None,
                  dtype: str = "bf16") -> None:

@@ -1,0 +1,102 @@
+"""Self-play training data from the on-device driver.
+
+``BatchedMCTS.selfplay_move(emit_targets=True)`` plays one move of every game on
+the GPU and emits that move's 8-fold targets (mcts.cpp:63-112). ``SelfPlayCollector``
+turns the stream of moves into the samples the reference's ``_self_play``
+returns (train.py:404-452) once a game is over: per move, 8 feature tensors
+``(1+2H, 8, 8)`` and 8 policy tensors ``(65,)``, and the value target of every
+sample = the final outcome (+1 black wins / -1 white wins / 0 draw, by disc
+count, train.py:438-445) from the perspective of the player to move at that
+step. For a game from the initial position that is exactly the reference's
+rule "+outcome for step 0, alternate sign every step, passes included"
+(train.py:447-450): players alternate every step, passes included. Games that
+start from a random opening get the same perspective rule, which the
+alternating form would get wrong when white moves first.
+
+The dict returned by ``add`` / ``drain`` has the reference's keys, so it feeds
+``_AlphaZeroDataset`` unchanged:
+    dataset.features += data["features"]; dataset.policies += data["policies"];
+    dataset.values += data["values"]
+"""
+
+from __future__ import annotations
+
+import torch
+
+# BatchedMCTS.selfplay_move "finished" codes (csrc/tree.hip k_selfplay_move)
+FIN_NONE, FIN_DRAW, FIN_BLACK, FIN_WHITE = 0, 1, 2, 3
+_OUTCOME_BLACK = {FIN_DRAW: 0.0, FIN_BLACK: 1.0, FIN_WHITE: -1.0}
+
+
+class SelfPlayCollector:
+    """Accumulates selfplay_move outputs per game; completed games become samples.
+
+    ``device``: where returned sample tensors live ("cpu" like the reference's
+    dataset, or a CUDA device to keep them in HBM)."""
+
+    def __init__(self, num_games: int, device: str | torch.device = "cpu") -> None:
+        self.num_games = num_games
+        self.device = torch.device(device)
+        self._moves: list[list[tuple[torch.Tensor, torch.Tensor]]] = [[] for _ in range(num_games)]
+        self._ready = {"features": [], "policies": [], "values": []}
+        self.games_completed = 0
+
+    def add(self, out: dict[str, torch.Tensor]) -> dict[str, list[torch.Tensor]]:
+        """Record one selfplay_move(emit_targets=True) result; return (and clear)
+        the samples of every game that finished on this move."""
+        if "features" not in out:
+            raise ValueError("selfplay_move must be called with emit_targets=True")
+        actions = out["actions"].to("cpu")
+        finished = out["finished"].to("cpu")
+        if actions.shape[0] != self.num_games:
+            raise ValueError(f"expected {self.num_games} games, got {actions.shape[0]}")
+        # the output buffers are reused by the next move: copy this move's targets
+        feats = out["features"].to(self.device, copy=True)
+        pols = out["policy"].to(self.device, copy=True)
+        for g in range(self.num_games):
+            if int(actions[g]) >= 0:  # a searched, expanded root: targets were written
+                self._moves[g].append((feats[g], pols[g]))
+            fin = int(finished[g])
+            if fin != FIN_NONE:
+                self._finish(g, _OUTCOME_BLACK[fin])
+        return self.drain()
+
+    def _finish(self, g: int, outcome_black: float) -> None:
+        for f8, p8 in self._moves[g]:
+            # plane 0 = player - 1: 0 when black is to move (transformation.h:83-116)
+            black_to_move = bool(f8[0, 0, 0, 0] == 0)
+            v = outcome_black if black_to_move else -outcome_black
+            for t in range(8):
+                self._ready["features"].append(f8[t])
+                self._ready["policies"].append(p8[t])
+                self._ready["values"].append(torch.tensor(v, dtype=torch.float32, device=self.device))
+        self._moves[g] = []
+        self.games_completed += 1
+
+    def drain(self) -> dict[str, list[torch.Tensor]]:
+        out = self._ready
+        self._ready = {"features": [], "policies": [], "values": []}
+        return out
+
+    def pending_moves(self, game: int) -> int:
+        return len(self._moves[game])
+
+
+def self_play(batched, neural_net, games: int, temperature_moves: int = 12, temperature: float = 1.0,
+              opening_moves: int = 0, device: str | torch.device = "cpu") -> dict[str, list[torch.Tensor]]:
+    """Play until ``games`` games have completed across the batch (each slot
+    restarts when its game ends) and return their samples in the reference's
+    ``_self_play`` format. ``opening_moves=0`` starts every game from the initial
+    position as train.py does."""
+    col = SelfPlayCollector(batched.num_games, device=device)
+    data = {"features": [], "policies": [], "values": []}
+    while col.games_completed < games:
+        batched.search(neural_net)
+        got = col.add(batched.selfplay_move(temperature_moves=temperature_moves, temperature=temperature,
+                                            opening_moves=opening_moves, emit_targets=True))
+        for k in data:
+            data[k] += got[k]
+    return data
+
+
+__all__ = ["SelfPlayCollector", "self_play", "FIN_NONE", "FIN_DRAW", "FIN_BLACK", "FIN_WHITE"]
