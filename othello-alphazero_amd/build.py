@@ -34,7 +34,9 @@ EXACT = ["-ffp-contract=off", "-fno-fast-math"]
 UNITS = {
     "tree.hip": EXACT,
     "capi.hip": EXACT,
-    "resnet.hip": [],
+    # accumulators and fragments in arch VGPRs: the default heuristic parks the
+    # 128 accumulators of a 1-wave/SIMD tile in AGPRs and shuffles them per MFMA
+    "resnet.hip": os.environ.get("OAMD_RESNET_FLAGS", "-mllvm -amdgpu-mfma-vgpr-form=1").split(),
 }
 
 

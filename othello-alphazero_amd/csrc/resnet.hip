@@ -49,14 +49,22 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-constexpr int kThreads = 512;
+// Output channels per wave (OAMD_WC): 64 -> 8 waves of 64ch x 64 positions,
+// 2 per SIMD; 128 -> 4 waves of 128ch x 64 positions, one per SIMD, with 0.375
+// instead of 0.5 fragment reads per MFMA.
+#ifndef OAMD_WC
+#define OAMD_WC 64
+#endif
+constexpr int kNT = OAMD_WC / 16;  // 16-channel MFMA tiles per wave
 constexpr int kLdsBytes = 160 * 1024;
 // Weight stage = 16 KiB (2 K-steps at C=128, 1 at C=256) in a 3-slot ring.
 // Compile-time schedule knobs, A/B-measured on MI355X with tools/ab.sh (same box,
 // k_resnet 8192 rows, C=128): 16 KiB stages beat 8 KiB stages in a 6-slot ring
 // (4 stages in flight) by 3 %; the per-step fence (OAMD_FENCE) gains 2 %;
 // forcing reads before MFMAs (OAMD_READS_FIRST), placing the DMA between MFMAs
-// (OAMD_DMA_LATE) and s_setprio around MFMA runs (OAMD_PRIO) each lose 1-4 %.
+// (OAMD_DMA_LATE) and s_setprio around MFMA runs (OAMD_PRIO) each lose 1-4 %;
+// issuing the activation fragments before the stage barrier (OAMD_XEARLY)
+// gains 3.6 %; 128-channel wave tiles (OAMD_WC=128, one wave per SIMD) lose 3 %.
 #ifndef OAMD_STAGE128
 #define OAMD_STAGE128 16384
 #endif
@@ -71,6 +79,9 @@ constexpr int kLdsBytes = 160 * 1024;
 #endif
 #ifndef OAMD_DMA_LATE
 #define OAMD_DMA_LATE 0
+#endif
+#ifndef OAMD_XEARLY
+#define OAMD_XEARLY 1
 #endif
 #ifndef OAMD_STAGGER
 #define OAMD_STAGGER 0
@@ -154,14 +165,16 @@ __constant__ TilePos kTilePos = make_tile_pos();
 template <int C>
 struct Geo {
     static constexpr int BOARDS = 512 / C;
-    static constexpr int WN = 8 / BOARDS;       // waves along output channels
+    static constexpr int WN = C / OAMD_WC;      // waves along output channels
+    static constexpr int WAVES = BOARDS * WN;
+    static constexpr int THREADS = WAVES * 64;
     static constexpr int RP = 2 * C + 16;       // row pitch (bytes)
     static constexpr int BROWS = 100;           // 10x10 padded board
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
     static constexpr int KS = ksteps_per_stage(C);
     static constexpr int KSTEP_BYTES = 32 * C * 2;
     static constexpr int STAGE = stage_bytes<C>();
-    static constexpr int DPT = STAGE / 16 / kThreads;        // DMAs per thread per stage
+    static constexpr int DPT = STAGE / 16 / THREADS;         // DMAs per thread per stage
     static constexpr int RING = (kLdsBytes - ACT_BYTES) / STAGE;  // weight ring slots
     static constexpr int LDS = ACT_BYTES + RING * STAGE;
     // The slot of stage s + RING - 2 is issued at the barrier that opens stage s,
@@ -169,6 +182,7 @@ struct Geo {
     static constexpr int VM_OPEN = (RING - 3) * DPT;   // vmcnt at a stage-opening barrier
     static constexpr int VM_LAYER = (RING - 2) * DPT;  // vmcnt after an epilogue's extra issue
     static_assert(RING >= 3 && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
+    static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 15, "decomposition");
 };
 
 template <int DT>
@@ -218,7 +232,7 @@ enum InputKind { kPacked = 0, kF32 = 1 };
 // Fragments of one K-step: 4 weight tiles (A: 16 channels x 32 K) and
 // 4 activation tiles (B: 32 K x 16 positions).
 struct Frags {
-    u32x4_t w[4];
+    u32x4_t w[kNT];
     u32x4_t x[4];
 };
 
@@ -240,33 +254,43 @@ __device__ __forceinline__ int kstep_offset(int i, bool first) {
 // ds_read the fragments of one K-step: wk = its weights in the ring (uniform),
 // aoff = kstep_offset (uniform); rd[m] / wl are per-lane bases
 template <int ABL = 0>
-__device__ __forceinline__ void load_frags(Frags& f, const unsigned char* act, const unsigned char* wk,
-                                           int aoff, const int (&rd)[4], int wl) {
+__device__ __forceinline__ void load_wfrags(Frags& f, const unsigned char* wk, int wl) {
     if constexpr (!(ABL & 4)) {
         const unsigned char* wp = wk + wl;
 #pragma unroll
-        for (int n = 0; n < 4; ++n) f.w[n] = *reinterpret_cast<const u32x4_t*>(wp + n * 1024);
+        for (int n = 0; n < kNT; ++n) f.w[n] = *reinterpret_cast<const u32x4_t*>(wp + n * 1024);
     }
+}
+
+template <int ABL = 0>
+__device__ __forceinline__ void load_xfrags(Frags& f, const unsigned char* act, int aoff, const int (&rd)[4]) {
     if constexpr (ABL & 2) return;
     const unsigned char* ap = act + aoff;
 #pragma unroll
     for (int m = 0; m < 4; ++m) f.x[m] = *reinterpret_cast<const u32x4_t*>(ap + rd[m]);
 }
 
+template <int ABL = 0>
+__device__ __forceinline__ void load_frags(Frags& f, const unsigned char* act, const unsigned char* wk,
+                                           int aoff, const int (&rd)[4], int wl) {
+    load_wfrags<ABL>(f, wk, wl);
+    load_xfrags<ABL>(f, act, aoff, rd);
+}
+
 // half h of a K-step's MFMAs: output channel tiles n = 2h, 2h+1
 template <int DT>
-__device__ __forceinline__ void mfma_half(f32x4_t (&acc)[4][4], const Frags& f, int h) {
+__device__ __forceinline__ void mfma_half(f32x4_t (&acc)[kNT][4], const Frags& f, int h) {
 #pragma unroll
-    for (int n = 2 * h; n < 2 * h + 2; ++n)
+    for (int n = h * kNT / 2; n < (h + 1) * kNT / 2; ++n)
 #pragma unroll
         for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
 }
 
 template <int DT>
-__device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[4][4], const Frags& f) {
+__device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[kNT][4], const Frags& f) {
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < kNT; ++n)
 #pragma unroll
         for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -283,7 +307,7 @@ __device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsig
     const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
     for (int i = 0; i < G::DPT; ++i) {
-        const int q = i * kThreads + wave * 64;  // first 16-byte chunk of this wave's piece
+        const int q = i * G::THREADS + wave * 64;  // first 16-byte chunk of this wave's piece
         __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
     }
 }
@@ -386,17 +410,18 @@ __device__ void heads(const NetView& N, const unsigned char* act, int wave, int 
 }
 
 template <int C>
-__device__ __forceinline__ void load_bias(float4 (&bv)[4], const NetView& N, int layer, int wn, int lane) {
+__device__ __forceinline__ void load_bias(float4 (&bv)[kNT], const NetView& N, int layer, int wn, int lane) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-        bv[n] = *reinterpret_cast<const float4*>(N.bias + (size_t)layer * C + wn * 64 + n * 16 + (lane >> 4) * 4);
+    for (int n = 0; n < kNT; ++n)
+        bv[n] = *reinterpret_cast<const float4*>(N.bias + (size_t)layer * C + wn * OAMD_WC + n * 16 +
+                                                 (lane >> 4) * 4);
 }
 
 // ABL != 0 only in diagnostic ablation builds (OAMD_RESNET_ABLATE, wrong results):
 // bit 0 = no in-loop barrier/DMA wait, 1 = no activation fragment reads,
 // 2 = no weight fragment reads, 3 = no in-loop weight DMA
 template <int C, int DT, int IN, int ABL = 0>
-__global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __restrict__ feat_in,
+__global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const void* __restrict__ feat_in,
                                                     int fw, int H, int rows,
                                                     float* __restrict__ policy,
                                                     float* __restrict__ value) {
@@ -409,7 +434,7 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
     const int wave = tid >> 6;
     const int lane = tid & 63;
     const int wm = wave / G::WN;  // board of this wave
-    const int wn = wave % G::WN;  // 64-channel block of this wave
+    const int wn = wave % G::WN;  // OAMD_WC-channel block of this wave
     const int kg = lane >> 4;
     const int row0 = blockIdx.x * G::BOARDS;
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
@@ -419,7 +444,7 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
 #pragma unroll
     for (int s = 0; s + 1 < G::RING; ++s) issue_stage_dma<C>(wsrc, ring, s, s, total, tid);
 
-    float4 bv[4];  // folded bias of this lane's 16 output channels (current layer)
+    float4 bv[kNT];  // folded bias of this lane's output channels (current layer)
     load_bias<C>(bv, N, 0, wn, lane);
 
     // per-lane bases: fragment reads (row of position tile m + k-group chunk),
@@ -429,12 +454,12 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
     for (int m = 0; m < 4; ++m) {
         const int rowb = (wm * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) * G::RP;
         rd[m] = rowb + kgroup_chunk(kg) * 16;
-        wr[m] = rowb + wn * 128 + kg * 8;
+        wr[m] = rowb + wn * OAMD_WC * 2 + kg * 8;
     }
-    const int wl = (wn * 4 * 64 + lane) * 16;
+    const int wl = (wn * kNT * 64 + lane) * 16;
 
     // ---------------- zero border rows; input planes -> channels 0..31 ------
-    for (int w = tid; w < G::BOARDS * 36 * (C / 8); w += kThreads) {
+    for (int w = tid; w < G::BOARDS * 36 * (C / 8); w += G::THREADS) {
         const int c = w % (C / 8), k = (w / (C / 8)) % 36, b = w / (C / 8) / 36;
         const int r = k < 10 ? k : (k < 20 ? 80 + k : ((k - 20) >> 1) * 10 + 10 + ((k & 1) ? 9 : 0));
         *reinterpret_cast<u32x4_t*>(act + (b * G::BROWS + r) * G::RP + c * 16) = u32x4_t{0u, 0u, 0u, 0u};
@@ -483,8 +508,8 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
                 u32x4_t{words[4 * c], words[4 * c + 1], words[4 * c + 2], words[4 * c + 3]};
     }
 
-    f32x4_t acc[4][4];
-    u32x2_t skip[4][4];  // residual (block input) of this lane's 64 outputs
+    f32x4_t acc[kNT][4];
+    u32x2_t skip[kNT][4];  // residual (block input) of this lane's outputs
 
     Frags fa, fb;
     int g = 0;     // stage holding the current K-step
@@ -506,7 +531,7 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
 
         // accumulators start at bias (+ block input for the block's second conv)
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int n = 0; n < kNT; ++n)
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 f32x4_t a = f32x4_t{bv[n].x, bv[n].y, bv[n].z, bv[n].w};
@@ -542,6 +567,10 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
                 mfma_half<DT>(acc, cur, 0);
                 __builtin_amdgcn_sched_barrier(0);
             }
+            // activation fragments do not depend on the stage barrier (the
+            // layer's input is fixed): with OAMD_XEARLY they are issued before
+            // it, so their latency overlaps the barrier wait
+            if constexpr (OAMD_XEARLY) load_xfrags<ABL>(nxt, act, kstep_offset<C>(i1, first), rd);
             int sp = 0;
             if constexpr (open) {
                 // open stage g+1: it has landed (this wave's DMAs, then everyone's
@@ -557,8 +586,8 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
                 slot = slot == G::RING - 1 ? 0 : slot + 1;
             }
             constexpr int kis = open ? 0 : 1;  // K-step within its stage
-            load_frags<ABL>(nxt, act, ring + slot * G::STAGE + kis * G::KSTEP_BYTES,
-                            kstep_offset<C>(i1, first), rd, wl);
+            load_wfrags<ABL>(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
+            if constexpr (!OAMD_XEARLY) load_xfrags<ABL>(nxt, act, kstep_offset<C>(i1, first), rd);
             if constexpr (open && !(ABL & 8) && OAMD_DMA_LATE)
                 issue_stage_dma<C>(wsrc, ring, g + G::RING - 2, sp, total, tid);
             if constexpr (gb) {
@@ -607,7 +636,7 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
         lds_barrier();  // every wave is done reading this layer's input and stage g
         issue_stage_dma<C>(wsrc, ring, g + G::RING - 1, slot == 0 ? G::RING - 1 : slot - 1, total, tid);
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int n = 0; n < kNT; ++n)
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 u32x2_t* p = reinterpret_cast<u32x2_t*>(act + wr[m] + n * 32);
@@ -629,7 +658,9 @@ __global__ __launch_bounds__(kThreads) void k_resnet(NetView N, const void* __re
         conv(std::integral_constant<int, 2>{}, 2 + 2 * blk);
     }
     __syncthreads();
-    heads<C, DT>(N, act, wave, lane, row0, rows, policy, value);
+    // (board, head) jobs: 2 per board, spread over the waves
+    for (int job = wave; job < 2 * G::BOARDS; job += G::WAVES)
+        heads<C, DT>(N, act, job, lane, row0, rows, policy, value);
 }
 
 template <int C, int DT, int IN, int ABL = 0>
@@ -643,7 +674,7 @@ static void launch_t(const NetView& N, const void* feat, int fw, int H, int rows
                                   hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         configured = true;
     }
-    hipLaunchKernelGGL((k_resnet<C, DT, IN, ABL>), dim3(grid), dim3(kThreads), G::LDS, s, N, feat, fw, H,
+    hipLaunchKernelGGL((k_resnet<C, DT, IN, ABL>), dim3(grid), dim3(G::THREADS), G::LDS, s, N, feat, fw, H,
                        rows, pol, val);
 }
 
