@@ -37,6 +37,10 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+# BASELINE.md "Published numbers for this path": the reference on 1x RTX 4090 +
+# 24-core CPU, 128x10b, history 8, 800 sims/move, 2 threads x 16 (README.md:25)
+PUBLISHED_SIMS_PER_S = 28000.0
 
 
 def resnet_flops_per_eval(in_ch: int, C: int, R: int, hidden: int) -> float:
@@ -164,6 +168,7 @@ def main() -> None:
     torch.cuda.synchronize()
     b.engine.enable_timing(True)
     ms0, launches0, rows0 = b.engine.nn_timing()
+    sel0, bk0, _ = b.engine.tree_timing()
 
     def run():
         for _ in range(args.steps):
@@ -171,6 +176,7 @@ def main() -> None:
 
     dt_max = timed_max(world, run, torch.cuda.synchronize, "cuda")
     ms1, launches1, rows1 = b.engine.nn_timing()
+    sel1, bk1, _ = b.engine.tree_timing()
     value = aggregate_rate(world, args.games, sims_per_search, args.steps, dt_max)
 
     nn_ms = ms1 - ms0
@@ -195,6 +201,27 @@ def main() -> None:
         except (ValueError, OSError):
             traffic = None
 
+    # tree kernels: latency-bound (one wave per game, dependent loads); HBM bytes
+    # per launch from the committed PMC summary of this workload, if present
+    tree_bytes = {}
+    tfile = ROOT / "profiles" / "traffic_tree.json"
+    if tfile.exists():
+        try:
+            tj = json.loads(tfile.read_text())
+            if tj.get("workload") == workload and tj.get("rows_per_launch") == int(rows_per_launch):
+                tree_bytes = {k: v["bytes_per_launch"] for k, v in tj["kernels"].items()}
+        except (ValueError, OSError, KeyError):
+            tree_bytes = {}
+    tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch)}
+    for name, ms in (("k_select", sel1 - sel0), ("k_backup", bk1 - bk0)):
+        avg = ms / max(1, nn_launches)
+        entry = {"avg_launch_ms": round(avg, 4)}
+        if name in tree_bytes:
+            gbs = tree_bytes[name] / (avg * 1e-3) / 1e9
+            entry.update({"hbm_bytes_per_launch": tree_bytes[name], "achieved_GB_s": round(gbs, 2),
+                          "frac_hbm_peak": round(gbs / PEAK_HBM_GBS, 5)})
+        tree[name] = entry
+
     result = {
         "metric": "MCTS simulations/sec (whole node), 800 sims/move, 128x10b ResNet, 1/2/4/8 GPU",
         "value": round(value, 1),
@@ -205,7 +232,9 @@ def main() -> None:
         "ms_per_step": round(dt_max * 1e3 / args.steps, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None,
+        "vs_baseline": round(value / PUBLISHED_SIMS_PER_S, 2),
+        "baseline_ref": {"value": PUBLISHED_SIMS_PER_S, "unit": "simulations/s",
+                         "hardware": "1x RTX 4090 + 24-core CPU (reference README.md:25, BASELINE.md)"},
         "dtype": args.dtype,
         "data": "synthetic: seeded random-init 128x10b AlphaZeroNet weights, random openings (0-8 plies)",
         "config": {
@@ -227,6 +256,7 @@ def main() -> None:
             "rows_per_launch": int(rows_per_launch),
             "flops_per_row": flops,
         },
+        "tree_kernels": tree,
     }
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.history, args.channels, R,

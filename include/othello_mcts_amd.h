@@ -230,6 +230,10 @@ int oamd_engine_game_key(oamd_engine *e, int32_t game, uint64_t *key_host);
 /* Timing of the last oamd_engine_search (HIP events on the engine stream):
  * total ms spent in the NN kernel, number of NN launches, rows evaluated. */
 int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches, int64_t *rows);
+/* Same for the tree kernels: total ms in k_select and in k_backup (one launch
+ * of each per NN launch). Timed searches record 5 HIP events per step and
+ * pipeline group on the group's stream. */
+int oamd_engine_tree_timing(const oamd_engine *e, float *select_ms, float *backup_ms, int64_t *launches);
 int oamd_engine_enable_timing(oamd_engine *e, int32_t enable);
 
 #ifdef __cplusplus

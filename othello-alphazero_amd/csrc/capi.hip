@@ -153,6 +153,8 @@ struct oamd_engine {
     bool timing = false;
     std::vector<hipEvent_t> ev;
     float nn_ms = 0.0f;
+    float select_ms = 0.0f;
+    float backup_ms = 0.0f;
     int64_t nn_launches = 0;
     int64_t nn_rows = 0;
 
@@ -723,6 +725,13 @@ int oamd_engine_nn_timing(const oamd_engine* e, float* nn_ms, int64_t* launches,
     return OAMD_OK;
 }
 
+int oamd_engine_tree_timing(const oamd_engine* e, float* select_ms, float* backup_ms, int64_t* launches) {
+    if (select_ms) *select_ms = e->select_ms;
+    if (backup_ms) *backup_ms = e->backup_ms;
+    if (launches) *launches = e->nn_launches;
+    return OAMD_OK;
+}
+
 int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* evals) {
     if (!net || !net->loaded) return fail(OAMD_INVALID_ARGUMENT, "native net not loaded");
     if (net->device != e->device) return fail(OAMD_INVALID_ARGUMENT, "net and engine on different devices");
@@ -743,7 +752,9 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     int rc = e->ensure_streams(K);
     if (rc) return rc;
     if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
-    const int nev = 2 * steps * K;
+    // timing: per (step, group) 5 events: select begin/end, NN begin (after the
+    // token wait)/end, backup end
+    const int nev = 5 * steps * K;
     while (e->timing && (int)e->ev.size() < nev) {
         hipEvent_t x;
         HIPCHK(hipEventCreate(&x));
@@ -763,17 +774,21 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     for (int s = 0; s < steps; ++s) {
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)g0[k] * L;
+            hipEvent_t* ev = e->timing ? &e->ev[5 * (s * K + k)] : nullptr;
+            if (ev) HIPCHK(hipEventRecord(ev[0], st[k]));
             launch_select(E, st[k], g0[k], ng[k]);
+            if (ev) HIPCHK(hipEventRecord(ev[1], st[k]));
             // NN launches of the groups run one after another (a token event):
             // each owns all CUs' MFMA pipes while the other groups' tree
             // kernels run beside it
             if (K > 1 && (s > 0 || k > 0)) HIPCHK(hipStreamWaitEvent(st[k], e->nn_token, 0));
-            if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * (s * K + k)], st[k]));
+            if (ev) HIPCHK(hipEventRecord(ev[2], st[k]));
             launch_resnet_packed(N, E.feat + r0 * E.FW, E.FW, E.H, ng[k] * L, E.policy + r0 * 65, E.value + r0,
                                  st[k]);
-            if (e->timing) HIPCHK(hipEventRecord(e->ev[2 * (s * K + k) + 1], st[k]));
+            if (ev) HIPCHK(hipEventRecord(ev[3], st[k]));
             if (K > 1) HIPCHK(hipEventRecord(e->nn_token, st[k]));
             launch_backup(E, st[k], g0[k], ng[k]);
+            if (ev) HIPCHK(hipEventRecord(ev[4], st[k]));
         }
     }
     LAUNCHCHK();
@@ -792,9 +807,14 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
         if (evals) *evals = (int64_t)c[1];
         if (e->timing) {
             for (int i = 0; i < steps * K; ++i) {
+                const hipEvent_t* ev = &e->ev[5 * i];
                 float ms = 0.0f;
-                HIPCHK(hipEventElapsedTime(&ms, e->ev[2 * i], e->ev[2 * i + 1]));
+                HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+                e->select_ms += ms;
+                HIPCHK(hipEventElapsedTime(&ms, ev[2], ev[3]));
                 e->nn_ms += ms;
+                HIPCHK(hipEventElapsedTime(&ms, ev[3], ev[4]));
+                e->backup_ms += ms;
             }
             e->nn_launches += (int64_t)steps * K;
             e->nn_rows += (int64_t)steps * e->G * L;

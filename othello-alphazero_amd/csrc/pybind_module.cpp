@@ -613,6 +613,12 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
             int64_t launches, rows;
             check(oamd_engine_nn_timing(e.h, &ms, &launches, &rows));
             return py::make_tuple(ms, launches, rows);
+        })
+        .def("tree_timing", [](Engine& e) {
+            float sel, bk;
+            int64_t launches;
+            check(oamd_engine_tree_timing(e.h, &sel, &bk, &launches));
+            return py::make_tuple(sel, bk, launches);
         });
 
     // GPU bitboard kernels over device buffers (data_ptr ints) for parity tests

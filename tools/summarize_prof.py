@@ -56,6 +56,19 @@ def main(tag: str) -> None:
             "workload": bench_line["config"]["workload"] if bench_line else None,
             "rows_per_launch": bench_line["roofline"]["rows_per_launch"] if bench_line else None,
             "note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> B), rocprofv3 --pmc, separate passes"}, indent=1))
+    tree = {}
+    for name in ("k_select", "k_backup"):
+        k = kern.get(name, {})
+        if "FETCH_SIZE_per_launch" in k and "WRITE_SIZE_per_launch" in k:
+            tree[name] = {"bytes_per_launch": round(2.0 * k["FETCH_SIZE_per_launch"] * 1024
+                                                    + k["WRITE_SIZE_per_launch"] * 1024),
+                          "avg_ns_rocprof": k.get("avg_ns")}
+    if tree:
+        (OUT / "traffic_tree.json").write_text(json.dumps({
+            "tag": tag, "kernels": tree,
+            "workload": bench_line["config"]["workload"] if bench_line else None,
+            "rows_per_launch": bench_line["roofline"]["rows_per_launch"] if bench_line else None,
+            "note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> B) per launch, rocprofv3 --pmc"}, indent=1))
     if "SQ_VALU_MFMA_BUSY_CYCLES_per_launch" in res and "GRBM_GUI_ACTIVE_per_launch" in res:
         # SQ_VALU_MFMA_BUSY_CYCLES sums MFMA-busy cycles over all SIMDs (1024 on MI355X);
         # GRBM_GUI_ACTIVE sums the GPU-active cycles over the 8 XCDs
