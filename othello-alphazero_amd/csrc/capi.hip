@@ -132,7 +132,6 @@ struct oamd_engine {
     float* value = nullptr;
     uint8_t* flags = nullptr;
     float* explore_tab = nullptr;
-    float* sqrt_tab = nullptr;
     unsigned long long* counters = nullptr;
     // query scratch
     oamd_root_info* info_dev = nullptr;
@@ -192,7 +191,6 @@ struct oamd_engine {
         E.policy = policy;
         E.value = value;
         E.explore_tab = explore_tab;
-        E.sqrt_tab = sqrt_tab;
         E.c_base = cfg.c_puct_base;
         E.c_init = cfg.c_puct_init;
         E.eps = cfg.dirichlet_epsilon;
@@ -228,13 +226,10 @@ struct oamd_engine {
     // exploration_rate table with the HOST's logf (bit-identical to the
     // reference's std::log(float), search_thread.cpp:198-203)
     int build_tables() {
-        std::vector<float> ex(kExploreTab), sq(kExploreTab);
-        for (int n = 0; n < kExploreTab; ++n) {
+        std::vector<float> ex(kExploreTab);
+        for (int n = 0; n < kExploreTab; ++n)
             ex[n] = std::log(((float)(1 + n) + cfg.c_puct_base) / cfg.c_puct_base) + cfg.c_puct_init;
-            sq[n] = std::sqrt((float)n);
-        }
         HIPCHK(hipMemcpy(explore_tab, ex.data(), ex.size() * sizeof(float), hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(sqrt_tab, sq.data(), sq.size() * sizeof(float), hipMemcpyHostToDevice));
         return OAMD_OK;
     }
 
@@ -253,7 +248,6 @@ struct oamd_engine {
         dfree(value);
         dfree(flags);
         dfree(explore_tab);
-        dfree(sqrt_tab);
         dfree(counters);
         dfree(info_dev);
         dfree(visits_dev);
@@ -594,8 +588,7 @@ int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity,
     e->seed = seed;
     const size_t nodes = (size_t)num_games * node_capacity;
     if ((rc = dalloc(&e->link, nodes)) || (rc = dalloc(&e->stat, nodes)) || (rc = dalloc(&e->pos, nodes)) ||
-        (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) ||
-        (rc = dalloc(&e->sqrt_tab, kExploreTab)) || (rc = dalloc(&e->counters, 2)) ||
+        (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) || (rc = dalloc(&e->counters, 2)) ||
         (rc = dalloc(&e->info_dev, num_games)) || (rc = dalloc(&e->visits_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->q_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->spd_dev, (size_t)8 * (1 + 2 * kMaxHistory) * 64 + 8 * 65)) || (rc = e->alloc_rows()) ||

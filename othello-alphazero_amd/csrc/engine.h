@@ -68,7 +68,6 @@ struct EngineView {
     float* policy;   // G*L*65
     float* value;    // G*L
     const float* explore_tab;  // kExploreTab
-    const float* sqrt_tab;     // kExploreTab
     float c_base, c_init, eps, alpha;
     unsigned long long* counters;  // [0] sims, [1] evals
 };

@@ -233,8 +233,13 @@ public:
             std::string s = b;
             std::memcpy(&seed, s.data(), 8);
         }
+        // one game owns the whole pool and nodes are not reclaimed during a game
+        // (DESIGN.md §5): default 2^23 nodes (512 MB) covers a full game at
+        // player.py's 3200 simulations per move (~1.6 M nodes)
+        if (node_capacity == 0) node_capacity = kSingleGameNodes;
         engine_ = std::make_unique<Engine>(device_, 1, node_capacity, c, seed);
     }
+    static constexpr int64_t kSingleGameNodes = (int64_t)1 << 23;
 
     void reset_position() {
         check(oamd_engine_reset(engine_->h, 0, next_seed()));

@@ -28,30 +28,47 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Wave reductions with DPP (row_shr / row_bcast inclusive scan, the total ends
+// in lane 63): a few cycles per step, where __shfl_xor compiles to a chain of
+// ds_bpermute LDS round trips (the dominant cost of a k_select level).
+template <int CTRL, int ROW_MASK, int BANK_MASK, typename T>
+__device__ __forceinline__ T dpp_move(T x, T id) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, id), __builtin_bit_cast(int, x),
+                                                             CTRL, ROW_MASK, BANK_MASK, false));
+}
+
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_scan_last(T v, T id, Op op) {
+    static_assert(sizeof(T) == 4, "32-bit lanes");
+    T t = op(v, dpp_move<0x111, 0xF, 0xF>(v, id));  // row_shr:1
+    t = op(t, dpp_move<0x112, 0xF, 0xF>(v, id));    // row_shr:2
+    t = op(t, dpp_move<0x113, 0xF, 0xF>(v, id));    // row_shr:3
+    t = op(t, dpp_move<0x114, 0xF, 0xE>(t, id));    // row_shr:4, banks 1-3
+    t = op(t, dpp_move<0x118, 0xF, 0xC>(t, id));    // row_shr:8, banks 2-3
+    t = op(t, dpp_move<0x142, 0xA, 0xF>(t, id));    // row_bcast:15 into rows 1, 3
+    t = op(t, dpp_move<0x143, 0xC, 0xF>(t, id));    // row_bcast:31 into rows 2, 3
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
+}
+
 __device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return v;
+    return wave_scan_last(v, 0, [](int a, int b) { return a + b; });
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
-    return v;
+    return wave_scan_last(v, -__builtin_inff(), [](float a, float b) { return fmaxf(a, b); });
 }
 
-// First index of the maximum (strict '>' scan in child order, search_thread.cpp:222,254).
-__device__ __forceinline__ int wave_argmax_first(float v, int idx) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float ov = __shfl_xor(v, off);
-        const int oi = __shfl_xor(idx, off);
-        if (ov > v || (ov == v && oi < idx)) {
-            v = ov;
-            idx = oi;
-        }
-    }
-    return idx;
+__device__ __forceinline__ int wave_max_i(int v) {
+    return wave_scan_last(v, (int)0x80000000, [](int a, int b) { return a > b ? a : b; });
+}
+
+// First lane holding the maximum (strict '>' scan in child order,
+// search_thread.cpp:222,254): the max, then the lowest lane equal to it.
+// Values are finite or -inf (no NaN).
+__device__ __forceinline__ int wave_argmax_first(float v, int) {
+    const float m = wave_max(v);
+    const uint64_t eq = __ballot(v == m);
+    return __ffsll((unsigned long long)eq) - 1;
 }
 
 __device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -108,10 +125,9 @@ __device__ __forceinline__ float explore_rate(const EngineView& E, int n) {
     return logf(((float)(1 + n) + E.c_base) / E.c_base) + E.c_init;
 }
 
-__device__ __forceinline__ float sqrt_count(const EngineView& E, int n) {
-    if (n >= 0 && n < kExploreTab) return E.sqrt_tab[n];
-    return sqrtf((float)n);
-}
+// sqrt of the children's visit sum: IEEE correctly rounded on the device as on
+// the host (HIP's default correctly-rounded fp32 sqrt, -fno-fast-math)
+__device__ __forceinline__ float sqrt_count(const EngineView&, int n) { return sqrtf((float)n); }
 
 // Square of the j-th legal action of a position (legal_actions order,
 // position.h:308-326), computed by lane = square.
@@ -203,27 +219,25 @@ __global__ __launch_bounds__(64) void k_select(EngineView E, int g0) {
         int p0 = lane == 0 ? root : -1;  // path slot `lane`
         int p1 = -1;                     // path slot 64 + lane
         NodeLink lk = root_link;
-        int node_n = root_n;  // visit count of `node` (parent N of the next choice)
+        // exploration rate of `node` (from its N); for a chosen child it was
+        // fetched by the child's lane at the previous level
+        float er = explore_rate(E, root_n);
         // One dependent memory round trip per level: the stats AND links of all
-        // children are loaded together; the chosen child's link and N come from
-        // its lane (readlane), not from a second load.
+        // children are loaded together; the chosen child's link, N and
+        // exploration rate come from its lane (readlane), not from a second load.
         while (!(lk.player == 0 || lk.n_children == 0) && d < kMaxDepth - 1) {
-            int child;
-            NodeLink clk;
-            int child_n;
-            if (lk.n_children == 1) {
-                child = lk.first_child;  // search_thread.cpp:194-196
-                clk = load_link(E.link + base + child);
-                child_n = E.stat[base + child].n;
-            } else {
-                const int nc = lk.n_children, fc = lk.first_child;
-                const float er = explore_rate(E, node_n);
-                NodeStat cs{0, 0.0f, 0.0f, 0.0f};
-                NodeLink cl{0, 0, 0, 0};
-                if (lane < nc) {
-                    cs = load_stat(E.stat + base + fc + lane);
-                    cl = load_link(E.link + base + fc + lane);
-                }
+            const int nc = lk.n_children, fc = lk.first_child;
+            int4 cs4 = make_int4(0, 0, 0, 0), cl4 = make_int4(0, 0, 0, 0);
+            if (lane < nc) {
+                cs4 = *reinterpret_cast<const int4*>(E.stat + base + fc + lane);
+                cl4 = *reinterpret_cast<const int4*>(E.link + base + fc + lane);
+            }
+            // every child lane fetches its own exploration rate now, so the
+            // chosen child's is ready for the next level (no dependent table read)
+            const float er_child = lane < nc ? explore_rate(E, cs4.x) : 0.0f;
+            int best = 0;
+            if (nc > 1) {
+                const NodeStat cs{cs4.x, __int_as_float(cs4.y), __int_as_float(cs4.z), __int_as_float(cs4.w)};
                 const int total = wave_sum(lane < nc ? cs.n : 0);
                 const float mult = er * sqrt_count(E, total);
                 float prob = cs.p;
@@ -241,20 +255,20 @@ __global__ __launch_bounds__(64) void k_select(EngineView E, int g0) {
                 }
                 float ucb = cs.q + mult * prob / (1.0f + (float)cs.n);
                 if (lane >= nc) ucb = -__builtin_inff();
-                const int best = wave_argmax_first(ucb, lane);
-                child = fc + best;
-                clk = NodeLink{readlane_i(cl.first_child, best), readlane_i(cl.n_children, best),
-                               readlane_i(cl.parent, best), readlane_i(cl.player, best)};
-                child_n = readlane_i(cs.n, best);
-            }
+                best = wave_argmax_first(ucb, lane);
+            }  // a single child is taken without scoring (search_thread.cpp:194-196)
+            const int child = fc + best;
+            const int4 clk4 = make_int4(readlane_i(cl4.x, best), readlane_i(cl4.y, best),
+                                        readlane_i(cl4.z, best), readlane_i(cl4.w, best));
+            const float er_next = readlane_f(er_child, best);
             ++d;
             if (lane == (d & 63)) {
                 if (d < 64) p0 = child;
                 else p1 = child;
             }
             node = child;
-            lk = clk;
-            node_n = child_n;
+            lk = NodeLink{clk4.x, clk4.y, clk4.z, clk4.w};
+            er = er_next;
         }
         if (d == kMaxDepth - 1 && lk.player != 0 && lk.n_children != 0 && lane == 0)
             atomicOr(&gs->flags, (int)kDepthCap);
@@ -293,7 +307,7 @@ __global__ __launch_bounds__(64) void k_select(EngineView E, int g0) {
         write_packed_features(E, base, r, d, p0, p1, hist_node, hist_n, lk.player, t, valid);
         sims += 1;
         evals += valid ? 1 : 0;
-        wait_stores();
+        wait_stores();  // the next descent reads these statistics
     }
     if (lane == 0) {
         gs->event = event;
@@ -714,8 +728,7 @@ __global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayPara
         } else {
             // argmax with uniform random tie-break (train.py:428-430)
             int m = n;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+            m = wave_max_i(m);
             const uint64_t ties = __ballot(lane < nc && n == m);
             const int nt = popcount64(ties);
             int k = (int)(u * (float)nt);

@@ -1,0 +1,22 @@
+#!/bin/bash
+# SQ counters of the tree kernels in the single-game latency run (one wave per
+# kernel): where a k_select / k_backup wave spends its cycles.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/tpmc
+timeout -k 10 300 rocprofv3 --pmc ${TREE_PMC:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM} \
+  -d gpurun_out/tpmc -o run --output-format csv -- python3 tools/latency.py > gpurun_out/tpmc/run.log 2>&1
+rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/tpmc/run.log; exit $rc; }
+python3 - <<'PY'
+import csv, glob
+from collections import defaultdict
+acc = defaultdict(lambda: defaultdict(list))
+for f in glob.glob("gpurun_out/tpmc/**/run_counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].split("(")[0].split()[-1]
+        if "k_select" in k or "k_backup" in k:
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, cs in acc.items():
+    print(k, {c: round(sum(v) / len(v)) for c, v in sorted(cs.items())})
+PY
