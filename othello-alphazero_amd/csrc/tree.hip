@@ -72,6 +72,10 @@ __device__ __forceinline__ int wave_argmax_first(float v, int) {
 }
 
 __device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
+}
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -327,97 +331,131 @@ __global__ __launch_bounds__(64) void k_backup(EngineView E, int g0) {
     GameState* gs = E.games + g;
     if (!(gs->flags & kActive)) return;
     const size_t base = (size_t)g * E.cap;
-    const int root = gs->root;
     int count = gs->count;
     bool overflow = false;
     __shared__ int expanded[kMaxLeaves];  // leaves expanded in this step, in order
     int n_expanded = 0;
 
-    for (int i = 0; i < E.L; ++i) {
-        const int r = g * E.L + i;
-        const int leaf = E.leaf[r];
-        const int d = E.depth[r];
-        const int t = E.trans[r];
-        const NodeLink lk = load_link(E.link + base + leaf);
-        // duplicate leaves of one step expand once (search_thread.cpp:133-135)
-        bool hit = false;
-        for (int k = lane; k < n_expanded; k += 64) hit |= expanded[k] == leaf;
-        const bool already = __any(hit);
-        if (lk.player != 0 && lk.n_children == 0 && !already) {
-            const Pos P = load_pos(E.pos + base + leaf, lk.player);
-            const int nc = P.legal ? popcount64(P.legal) : 1;
-            if ((int64_t)count + nc > E.cap) {
-                overflow = true;  // leaf stays a leaf; value still backed up
-            } else {
-                const int fc = count;
-                count += nc;
-                const float* pol = E.policy + (size_t)r * 65;
-                int action = -1, j = 0;
-                if (P.legal) {
-                    const int s = lane;
-                    if ((P.legal >> (63 - s)) & 1ULL) {
-                        action = s;
-                        j = s == 0 ? 0 : popcount64(P.legal & (~0ULL << (64 - s)));
+    // Leaves are processed in order (their backups share path nodes), but
+    // everything a leaf needs except the path statistics is independent of
+    // the earlier leaves of the step: it is fetched for 64 leaves at once, one
+    // lane per leaf (a duplicate leaf's link may be stale after its first copy
+    // expanded it; duplicates never expand again and only use the player).
+    for (int c0 = 0; c0 < E.L; c0 += 64) {
+        const int cl = c0 + lane < E.L ? lane : 0;
+        const int rl = g * E.L + c0 + cl;
+        const int leaf_v = E.leaf[rl];
+        const int d_v = E.depth[rl];
+        const int t_v = E.trans[rl];
+        const float val_v = E.value[rl];
+        const int4 lk_v = *reinterpret_cast<const int4*>(E.link + base + leaf_v);
+        const NodePos pos_v = E.pos[base + leaf_v];
+        const int cend = E.L - c0 < 64 ? E.L - c0 : 64;
+        // path of the chunk's first leaf; each leaf prefetches the next one's
+        int gp0 = 0, gp1 = 0;
+        {
+            const int* gp = E.path + (size_t)(g * E.L + c0) * kMaxDepth;
+            const int d0 = readlane_i(d_v, 0);
+            if (lane >= 1 && lane <= d0) gp0 = gp[lane];
+            if (64 + lane <= d0) gp1 = gp[64 + lane];
+        }
+        for (int j = 0; j < cend; ++j) {
+            const int r = g * E.L + c0 + j;
+            const int leaf = readlane_i(leaf_v, j);
+            const int d = readlane_i(d_v, j);
+            const int t = readlane_i(t_v, j);
+            const NodeLink lk{readlane_i(lk_v.x, j), readlane_i(lk_v.y, j), readlane_i(lk_v.z, j),
+                              readlane_i(lk_v.w, j)};
+            const int path0 = gp0, path1 = gp1;
+            if (j + 1 < cend) {  // next leaf's path, behind this leaf's work
+                const int* gp = E.path + (size_t)(r + 1) * kMaxDepth;
+                const int dn = readlane_i(d_v, j + 1);
+                if (lane >= 1 && lane <= dn) gp0 = gp[lane];
+                if (64 + lane <= dn) gp1 = gp[64 + lane];
+            }
+            // duplicate leaves of one step expand once (search_thread.cpp:133-135)
+            bool hit = false;
+            for (int k = lane; k < n_expanded; k += 64) hit |= expanded[k] == leaf;
+            const bool already = __any(hit);
+            if (lk.player != 0 && lk.n_children == 0 && !already) {
+                Pos P;
+                P.player = lk.player;
+                P.pad_ = 0;
+                P.p1 = readlane_u64(pos_v.p1, j);
+                P.p2 = readlane_u64(pos_v.p2, j);
+                P.legal = readlane_u64(pos_v.legal, j);
+                P.next_legal = readlane_u64(pos_v.next_legal, j);
+                const int nc = P.legal ? popcount64(P.legal) : 1;
+                if ((int64_t)count + nc > E.cap) {
+                    overflow = true;  // leaf stays a leaf; value still backed up
+                } else {
+                    const int fc = count;
+                    count += nc;
+                    const float* pol = E.policy + (size_t)r * 65;
+                    int action = -1, jj = 0;
+                    if (P.legal) {
+                        const int sq = lane;
+                        if ((P.legal >> (63 - sq)) & 1ULL) {
+                            action = sq;
+                            jj = sq == 0 ? 0 : popcount64(P.legal & (~0ULL << (64 - sq)));
+                        }
+                    } else if (lane == 0) {
+                        action = 64;
+                        jj = 0;
                     }
-                } else if (lane == 0) {
-                    action = 64;
-                    j = 0;
+                    if (action >= 0) {
+                        const Pos c = apply_action(P, action);
+                        const int id = fc + jj;
+                        store_link(E.link + base + id, NodeLink{-1, 0, leaf, c.player});
+                        store_stat(E.stat + base + id,
+                                   NodeStat{0, 0.0f, 0.0f, pol[transform_action(action, t)]});
+                        store_pos(E.pos + base + id, c);
+                    }
+                    if (lane == 0) store_link(E.link + base + leaf, NodeLink{fc, nc, lk.parent, lk.player});
+                    if (lane == 0) expanded[n_expanded] = leaf;
+                    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS write visible to the wave
+                    __builtin_amdgcn_wave_barrier();
+                    ++n_expanded;
                 }
-                if (action >= 0) {
-                    const Pos c = apply_action(P, action);
-                    const int id = fc + j;
-                    store_link(E.link + base + id, NodeLink{-1, 0, leaf, c.player});
-                    store_stat(E.stat + base + id,
-                               NodeStat{0, 0.0f, 0.0f, pol[transform_action(action, t)]});
-                    store_pos(E.pos + base + id, c);
+            }
+            if (d > 0) {
+                float v;
+                if (lk.player != 0) {
+                    v = -readlane_f(val_v, j);
+                } else {
+                    // terminal: score from the perspective of the parent's player
+                    const NodeLink pl = load_link(E.link + base + lk.parent);
+                    const uint64_t lp1 = readlane_u64(pos_v.p1, j);
+                    const uint64_t lp2 = readlane_u64(pos_v.p2, j);
+                    const uint64_t mine = pl.player == 1 ? lp1 : lp2;
+                    const uint64_t theirs = pl.player == 1 ? lp2 : lp1;
+                    const int a = popcount64(mine), b = popcount64(theirs);
+                    v = a > b ? 1.0f : (a < b ? -1.0f : 0.0f);
                 }
-                if (lane == 0) store_link(E.link + base + leaf, NodeLink{fc, nc, lk.parent, lk.player});
-                if (lane == 0) expanded[n_expanded] = leaf;
-                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS write visible to the wave
-                __builtin_amdgcn_wave_barrier();
-                ++n_expanded;
+                // node at depth k receives v * (-1)^(d-k)  (sign flips walking up)
+                if (lane >= 1 && lane <= d) {
+                    const float vk = ((d - lane) & 1) ? -v : v;
+                    NodeStat s = load_stat(E.stat + base + path0);
+                    s.w += 1.0f + vk;
+                    s.q = s.w / (float)s.n;
+                    store_stat(E.stat + base + path0, s);
+                }
+                if (64 + lane <= d) {
+                    const int k = 64 + lane;
+                    const float vk = ((d - k) & 1) ? -v : v;
+                    NodeStat s = load_stat(E.stat + base + path1);
+                    s.w += 1.0f + vk;
+                    s.q = s.w / (float)s.n;
+                    store_stat(E.stat + base + path1, s);
+                }
             }
+            wait_stores();  // the next leaf's backup reads these statistics
         }
-        if (d > 0) {
-            float v;
-            if (lk.player != 0) {
-                v = -E.value[r];
-            } else {
-                // terminal: score from the perspective of the parent's player
-                const NodeLink pl = load_link(E.link + base + lk.parent);
-                const NodePos lp = E.pos[base + leaf];
-                const uint64_t mine = pl.player == 1 ? lp.p1 : lp.p2;
-                const uint64_t theirs = pl.player == 1 ? lp.p2 : lp.p1;
-                const int a = popcount64(mine), b = popcount64(theirs);
-                v = a > b ? 1.0f : (a < b ? -1.0f : 0.0f);
-            }
-            const int* gp = E.path + (size_t)r * kMaxDepth;
-            // node at depth k receives v * (-1)^(d-k)  (sign flips walking up)
-            if (lane >= 1 && lane <= d) {
-                const int node = gp[lane];
-                const float vk = ((d - lane) & 1) ? -v : v;
-                NodeStat s = load_stat(E.stat + base + node);
-                s.w += 1.0f + vk;
-                s.q = s.w / (float)s.n;
-                store_stat(E.stat + base + node, s);
-            }
-            if (64 + lane <= d) {
-                const int k = 64 + lane;
-                const int node = gp[k];
-                const float vk = ((d - k) & 1) ? -v : v;
-                NodeStat s = load_stat(E.stat + base + node);
-                s.w += 1.0f + vk;
-                s.q = s.w / (float)s.n;
-                store_stat(E.stat + base + node, s);
-            }
-        }
-        wait_stores();
     }
     if (lane == 0) {
         gs->count = count;
         if (overflow) gs->flags |= kOverflow;
     }
-    (void)root;
 }
 
 // ---------------------------------------------------------------------------
