@@ -55,7 +55,6 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 #ifndef OAMD_WC
 #define OAMD_WC 64
 #endif
-constexpr int kNT = OAMD_WC / 16;  // 16-channel MFMA tiles per wave
 constexpr int kLdsBytes = 160 * 1024;
 // Weight stage = 16 KiB (2 K-steps at C=128, 1 at C=256) in a 3-slot ring.
 // Compile-time schedule knobs, A/B-measured on MI355X with tools/ab.sh (same box,
@@ -162,10 +161,15 @@ constexpr TilePos make_tile_pos() {
 }
 __constant__ TilePos kTilePos = make_tile_pos();
 
-template <int C>
-struct Geo {
-    static constexpr int BOARDS = 512 / C;
-    static constexpr int WN = C / OAMD_WC;      // waves along output channels
+// Workgroup geometry: C channels, BOARDS boards per workgroup, WC output
+// channels per wave (NT = WC/16 MFMA tiles), at most RING_MAX weight slots.
+template <int C_, int BOARDS_, int WC_, int RING_MAX_>
+struct GeoT {
+    static constexpr int C = C_;
+    static constexpr int BOARDS = BOARDS_;
+    static constexpr int WC = WC_;
+    static constexpr int NT = WC / 16;
+    static constexpr int WN = C / WC;           // waves along output channels
     static constexpr int WAVES = BOARDS * WN;
     static constexpr int THREADS = WAVES * 64;
     static constexpr int RP = 2 * C + 16;       // row pitch (bytes)
@@ -175,15 +179,28 @@ struct Geo {
     static constexpr int KSTEP_BYTES = 32 * C * 2;
     static constexpr int STAGE = stage_bytes<C>();
     static constexpr int DPT = STAGE / 16 / THREADS;         // DMAs per thread per stage
-    static constexpr int RING = (kLdsBytes - ACT_BYTES) / STAGE;  // weight ring slots
+    static constexpr int RING_FIT = (kLdsBytes - ACT_BYTES) / STAGE;
+    static constexpr int RING = RING_FIT < RING_MAX_ ? RING_FIT : RING_MAX_;  // weight ring slots
     static constexpr int LDS = ACT_BYTES + RING * STAGE;
     // The slot of stage s + RING - 2 is issued at the barrier that opens stage s,
     // so RING - 2 stages are in flight while one is read.
     static constexpr int VM_OPEN = (RING - 3) * DPT;   // vmcnt at a stage-opening barrier
     static constexpr int VM_LAYER = (RING - 2) * DPT;  // vmcnt after an epilogue's extra issue
     static_assert(RING >= 3 && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
-    static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 15, "decomposition");
+    static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 63, "decomposition");
 };
+// throughput geometry: 512 positions x C channels per workgroup, 8 waves
+template <int C>
+using Geo = GeoT<C, 512 / C, OAMD_WC, 3>;
+// small-batch geometry (latency): one board per workgroup, 4 waves of C/4
+// channels, so a handful of rows spreads over as many CUs as boards; the LDS
+// ring depth (4, 6 or 8 slots) measured equal: at 8 MFMAs per wave and K-step
+// the per-step synchronisation, not the weight stream, bounds this geometry
+#ifndef OAMD_SMALL_RING
+#define OAMD_SMALL_RING 4
+#endif
+template <int C>
+using GeoS = GeoT<C, 1, C / 4, OAMD_SMALL_RING>;
 
 template <int DT>
 __device__ __forceinline__ uint32_t to_act(float v) {
@@ -231,8 +248,9 @@ enum InputKind { kPacked = 0, kF32 = 1 };
 
 // Fragments of one K-step: 4 weight tiles (A: 16 channels x 32 K) and
 // 4 activation tiles (B: 32 K x 16 positions).
+template <int NT>
 struct Frags {
-    u32x4_t w[kNT];
+    u32x4_t w[NT];
     u32x4_t x[4];
 };
 
@@ -253,44 +271,44 @@ __device__ __forceinline__ int kstep_offset(int i, bool first) {
 
 // ds_read the fragments of one K-step: wk = its weights in the ring (uniform),
 // aoff = kstep_offset (uniform); rd[m] / wl are per-lane bases
-template <int ABL = 0>
-__device__ __forceinline__ void load_wfrags(Frags& f, const unsigned char* wk, int wl) {
+template <int ABL = 0, int NT>
+__device__ __forceinline__ void load_wfrags(Frags<NT>& f, const unsigned char* wk, int wl) {
     if constexpr (!(ABL & 4)) {
         const unsigned char* wp = wk + wl;
 #pragma unroll
-        for (int n = 0; n < kNT; ++n) f.w[n] = *reinterpret_cast<const u32x4_t*>(wp + n * 1024);
+        for (int n = 0; n < NT; ++n) f.w[n] = *reinterpret_cast<const u32x4_t*>(wp + n * 1024);
     }
 }
 
-template <int ABL = 0>
-__device__ __forceinline__ void load_xfrags(Frags& f, const unsigned char* act, int aoff, const int (&rd)[4]) {
+template <int ABL = 0, int NT>
+__device__ __forceinline__ void load_xfrags(Frags<NT>& f, const unsigned char* act, int aoff, const int (&rd)[4]) {
     if constexpr (ABL & 2) return;
     const unsigned char* ap = act + aoff;
 #pragma unroll
     for (int m = 0; m < 4; ++m) f.x[m] = *reinterpret_cast<const u32x4_t*>(ap + rd[m]);
 }
 
-template <int ABL = 0>
-__device__ __forceinline__ void load_frags(Frags& f, const unsigned char* act, const unsigned char* wk,
+template <int ABL = 0, int NT>
+__device__ __forceinline__ void load_frags(Frags<NT>& f, const unsigned char* act, const unsigned char* wk,
                                            int aoff, const int (&rd)[4], int wl) {
     load_wfrags<ABL>(f, wk, wl);
     load_xfrags<ABL>(f, act, aoff, rd);
 }
 
 // half h of a K-step's MFMAs: output channel tiles n = 2h, 2h+1
-template <int DT>
-__device__ __forceinline__ void mfma_half(f32x4_t (&acc)[kNT][4], const Frags& f, int h) {
+template <int DT, int NT>
+__device__ __forceinline__ void mfma_half(f32x4_t (&acc)[NT][4], const Frags<NT>& f, int h) {
 #pragma unroll
-    for (int n = h * kNT / 2; n < (h + 1) * kNT / 2; ++n)
+    for (int n = h * NT / 2; n < (h + 1) * NT / 2; ++n)
 #pragma unroll
         for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
 }
 
-template <int DT>
-__device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[kNT][4], const Frags& f) {
+template <int DT, int NT>
+__device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[NT][4], const Frags<NT>& f) {
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int n = 0; n < kNT; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
         for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -298,10 +316,9 @@ __device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[kNT][4], const Frags& 
 
 // Stages past the last one re-read the last stage into a slot nobody reads any
 // more: the issue stays branch-free and the vmcnt bookkeeping uniform.
-template <int C>
+template <class G>
 __device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsigned char* ring, int g, int slot,
                                                 int total, int tid) {
-    using G = Geo<C>;
     const unsigned char* src = wsrc + (size_t)(g < total ? g : total - 1) * G::STAGE;
     unsigned char* dst = ring + slot * G::STAGE;
     const int wave = tid >> 6, lane = tid & 63;
@@ -316,8 +333,8 @@ __device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsig
 // (gfx9 encoding: vmcnt[3:0], expcnt[6:4] = 7, lgkmcnt[11:8] = 15: no wait on those)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-    static_assert(N >= 0 && N < 16, "vmcnt");
-    __builtin_amdgcn_s_waitcnt(N | 0x0F70);
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);  // vmcnt[3:0], vmcnt[5:4] at 15:14
     asm volatile("" ::: "memory");
 }
 
@@ -329,10 +346,10 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
-template <int C, int DT>
+template <class G, int DT>
 __device__ void heads(const NetView& N, const unsigned char* act, int wave, int lane, int row0, int rows,
                       float* __restrict__ policy, float* __restrict__ value) {
-    using G = Geo<C>;
+    constexpr int C = G::C;
     constexpr int BOARDS = G::BOARDS;
     const HeadLayout HL(C, N.hidden);
     const float* hp = N.head;
@@ -409,23 +426,24 @@ __device__ void heads(const NetView& N, const unsigned char* act, int wave, int 
     }
 }
 
-template <int C>
-__device__ __forceinline__ void load_bias(float4 (&bv)[kNT], const NetView& N, int layer, int wn, int lane) {
+template <class G>
+__device__ __forceinline__ void load_bias(float4 (&bv)[G::NT], const NetView& N, int layer, int wn, int lane) {
 #pragma unroll
-    for (int n = 0; n < kNT; ++n)
-        bv[n] = *reinterpret_cast<const float4*>(N.bias + (size_t)layer * C + wn * OAMD_WC + n * 16 +
+    for (int n = 0; n < G::NT; ++n)
+        bv[n] = *reinterpret_cast<const float4*>(N.bias + (size_t)layer * G::C + wn * G::WC + n * 16 +
                                                  (lane >> 4) * 4);
 }
 
 // ABL != 0 only in diagnostic ablation builds (OAMD_RESNET_ABLATE, wrong results):
 // bit 0 = no in-loop barrier/DMA wait, 1 = no activation fragment reads,
 // 2 = no weight fragment reads, 3 = no in-loop weight DMA
-template <int C, int DT, int IN, int ABL = 0>
-__global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const void* __restrict__ feat_in,
+template <class G, int DT, int IN, int ABL = 0>
+__global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __restrict__ feat_in,
                                                     int fw, int H, int rows,
                                                     float* __restrict__ policy,
                                                     float* __restrict__ value) {
-    using G = Geo<C>;
+    constexpr int C = G::C;
+    constexpr int kNT = G::NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* act = smem;
     unsigned char* ring = smem + G::ACT_BYTES;
@@ -442,10 +460,10 @@ __global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const voi
 
     // weight stream starts right away: stages 0 .. RING-2
 #pragma unroll
-    for (int s = 0; s + 1 < G::RING; ++s) issue_stage_dma<C>(wsrc, ring, s, s, total, tid);
+    for (int s = 0; s + 1 < G::RING; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
 
     float4 bv[kNT];  // folded bias of this lane's output channels (current layer)
-    load_bias<C>(bv, N, 0, wn, lane);
+    load_bias<G>(bv, N, 0, wn, lane);
 
     // per-lane bases: fragment reads (row of position tile m + k-group chunk),
     // epilogue writes (row + k-group's 8-byte half chunk), weight fragments
@@ -454,7 +472,7 @@ __global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const voi
     for (int m = 0; m < 4; ++m) {
         const int rowb = (wm * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) * G::RP;
         rd[m] = rowb + kgroup_chunk(kg) * 16;
-        wr[m] = rowb + wn * OAMD_WC * 2 + kg * 8;
+        wr[m] = rowb + wn * G::WC * 2 + kg * 8;
     }
     const int wl = (wn * kNT * 64 + lane) * 16;
 
@@ -511,7 +529,7 @@ __global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const voi
     f32x4_t acc[kNT][4];
     u32x2_t skip[kNT][4];  // residual (block input) of this lane's outputs
 
-    Frags fa, fb;
+    Frags<kNT> fa, fb;
     int g = 0;     // stage holding the current K-step
     int slot = 0;  // g % RING
 
@@ -550,7 +568,7 @@ __global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const voi
         // GB = waves 4-7 (the SIMD partners of waves 0-3) with OAMD_STAGGER: half
         // of cur's MFMAs go before the barrier, so while waves 0-3 issue the
         // post-barrier DMA and reads, their partners keep the MFMA pipe busy
-        auto step = [&](auto NEW, auto GB, const Frags& cur, Frags& nxt, int i1) {
+        auto step = [&](auto NEW, auto GB, const Frags<kNT>& cur, Frags<kNT>& nxt, int i1) {
             constexpr bool open = decltype(NEW)::value;
             constexpr bool gb = decltype(GB)::value;
 #if OAMD_FENCE
@@ -581,7 +599,7 @@ __global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const voi
                 }
                 sp = slot == 0 ? G::RING - 1 : slot - 1;  // (g + RING - 1) % RING
                 if constexpr (!(ABL & 8) && !OAMD_DMA_LATE)
-                    issue_stage_dma<C>(wsrc, ring, g + G::RING - 1, sp, total, tid);
+                    issue_stage_dma<G>(wsrc, ring, g + G::RING - 1, sp, total, tid);
                 ++g;
                 slot = slot == G::RING - 1 ? 0 : slot + 1;
             }
@@ -589,7 +607,7 @@ __global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const voi
             load_wfrags<ABL>(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
             if constexpr (!OAMD_XEARLY) load_xfrags<ABL>(nxt, act, kstep_offset<C>(i1, first), rd);
             if constexpr (open && !(ABL & 8) && OAMD_DMA_LATE)
-                issue_stage_dma<C>(wsrc, ring, g + G::RING - 2, sp, total, tid);
+                issue_stage_dma<G>(wsrc, ring, g + G::RING - 2, sp, total, tid);
             if constexpr (gb) {
                 mfma_half<DT>(acc, cur, 1);
             } else {
@@ -632,9 +650,9 @@ __global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const voi
         // stages g+1 .. (next layer's) are in flight; the next layer's bias is
         // loaded before the next DMA so the counted wait below covers it
         const bool more = layer + 1 < nlayers;
-        if (more) load_bias<C>(bv, N, layer + 1, wn, lane);
+        if (more) load_bias<G>(bv, N, layer + 1, wn, lane);
         lds_barrier();  // every wave is done reading this layer's input and stage g
-        issue_stage_dma<C>(wsrc, ring, g + G::RING - 1, slot == 0 ? G::RING - 1 : slot - 1, total, tid);
+        issue_stage_dma<G>(wsrc, ring, g + G::RING - 1, slot == 0 ? G::RING - 1 : slot - 1, total, tid);
 #pragma unroll
         for (int n = 0; n < kNT; ++n)
 #pragma unroll
@@ -660,21 +678,20 @@ __global__ __launch_bounds__(Geo<C>::THREADS) void k_resnet(NetView N, const voi
     __syncthreads();
     // (board, head) jobs: 2 per board, spread over the waves
     for (int job = wave; job < 2 * G::BOARDS; job += G::WAVES)
-        heads<C, DT>(N, act, job, lane, row0, rows, policy, value);
+        heads<G, DT>(N, act, job, lane, row0, rows, policy, value);
 }
 
-template <int C, int DT, int IN, int ABL = 0>
+template <class G, int DT, int IN, int ABL = 0>
 static void launch_t(const NetView& N, const void* feat, int fw, int H, int rows, float* pol,
                      float* val, hipStream_t s) {
-    using G = Geo<C>;
     const unsigned grid = (unsigned)((rows + G::BOARDS - 1) / G::BOARDS);
     static bool configured = false;
     if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_resnet<C, DT, IN, ABL>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_resnet<G, DT, IN, ABL>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
         configured = true;
     }
-    hipLaunchKernelGGL((k_resnet<C, DT, IN, ABL>), dim3(grid), dim3(G::THREADS), G::LDS, s, N, feat, fw, H,
+    hipLaunchKernelGGL((k_resnet<G, DT, IN, ABL>), dim3(grid), dim3(G::THREADS), G::LDS, s, N, feat, fw, H,
                        rows, pol, val);
 }
 
@@ -688,6 +705,11 @@ static int ablation() {
 }
 #endif
 
+#ifndef OAMD_SMALL_BATCH_ROWS
+#define OAMD_SMALL_BATCH_ROWS 1024
+#endif
+constexpr int kSmallBatchRows = OAMD_SMALL_BATCH_ROWS;
+
 template <int IN>
 static void dispatch(const NetView& N, const void* feat, int fw, int H, int rows, float* pol,
                      float* val, hipStream_t s) {
@@ -696,24 +718,39 @@ static void dispatch(const NetView& N, const void* feat, int fw, int H, int rows
     if constexpr (IN == kF32) {
         if (N.C == 128 && N.dtype == OAMD_BF16 && ablation()) {
             switch (ablation()) {
-                case 1: return launch_t<128, OAMD_BF16, IN, 1>(N, feat, fw, H, rows, pol, val, s);
-                case 2: return launch_t<128, OAMD_BF16, IN, 2>(N, feat, fw, H, rows, pol, val, s);
-                case 4: return launch_t<128, OAMD_BF16, IN, 4>(N, feat, fw, H, rows, pol, val, s);
-                case 6: return launch_t<128, OAMD_BF16, IN, 6>(N, feat, fw, H, rows, pol, val, s);
-                case 8: return launch_t<128, OAMD_BF16, IN, 8>(N, feat, fw, H, rows, pol, val, s);
-                case 9: return launch_t<128, OAMD_BF16, IN, 9>(N, feat, fw, H, rows, pol, val, s);
-                case 15: return launch_t<128, OAMD_BF16, IN, 15>(N, feat, fw, H, rows, pol, val, s);
+                case 1: return launch_t<Geo<128>, OAMD_BF16, IN, 1>(N, feat, fw, H, rows, pol, val, s);
+                case 2: return launch_t<Geo<128>, OAMD_BF16, IN, 2>(N, feat, fw, H, rows, pol, val, s);
+                case 4: return launch_t<Geo<128>, OAMD_BF16, IN, 4>(N, feat, fw, H, rows, pol, val, s);
+                case 6: return launch_t<Geo<128>, OAMD_BF16, IN, 6>(N, feat, fw, H, rows, pol, val, s);
+                case 8: return launch_t<Geo<128>, OAMD_BF16, IN, 8>(N, feat, fw, H, rows, pol, val, s);
+                case 9: return launch_t<Geo<128>, OAMD_BF16, IN, 9>(N, feat, fw, H, rows, pol, val, s);
+                case 15: return launch_t<Geo<128>, OAMD_BF16, IN, 15>(N, feat, fw, H, rows, pol, val, s);
                 default: break;
             }
         }
     }
 #endif
+    // Below kSmallBatchRows rows the throughput geometry would leave most CUs
+    // idle and its per-workgroup latency (4 or 2 boards through the whole tower)
+    // sets the call's latency: one board per workgroup instead. The K order and
+    // MFMA tiling per output are the same, so results are bit-identical.
+    const bool small = rows < kSmallBatchRows;
     if (N.C == 128) {
-        if (N.dtype == OAMD_FP16) launch_t<128, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
-        else launch_t<128, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+        if (small) {
+            if (N.dtype == OAMD_FP16) launch_t<GeoS<128>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
+            else launch_t<GeoS<128>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+        } else {
+            if (N.dtype == OAMD_FP16) launch_t<Geo<128>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
+            else launch_t<Geo<128>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+        }
     } else {
-        if (N.dtype == OAMD_FP16) launch_t<256, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
-        else launch_t<256, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+        if (small) {
+            if (N.dtype == OAMD_FP16) launch_t<GeoS<256>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
+            else launch_t<GeoS<256>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+        } else {
+            if (N.dtype == OAMD_FP16) launch_t<Geo<256>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
+            else launch_t<Geo<256>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+        }
     }
 }
 

@@ -147,3 +147,20 @@ def test_pipeline_groups_do_not_change_results(om):
         b.search(net)
         runs.append([(b.visit_counts(g), b.mean_action_values(g)) for g in range(12)])
     assert runs[0] == runs[1] == runs[2]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("C,R", [(128, 9), (256, 3)])
+def test_small_batch_geometry_is_bit_identical(om, dtype, C, R):
+    """Fewer than 1024 rows run one board per workgroup (latency geometry);
+    the K order per output is unchanged, so rows evaluated alone match the
+    same rows inside a large (throughput-geometry) batch bit for bit."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(11, 17, C, R, 64), device=0, dtype=dtype)
+    gen = torch.Generator().manual_seed(C)
+    x = (torch.rand((1100, 17, 8, 8), generator=gen) < 0.3).float().to(DEV)
+    big = net(x)
+    small = net(x[:100].contiguous())
+    assert torch.equal(big["policy"][:100], small["policy"])
+    assert torch.equal(big["value"][:100], small["value"])
