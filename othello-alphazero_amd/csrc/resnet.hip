@@ -296,6 +296,15 @@ __device__ __forceinline__ void load_frags(Frags<NT>& f, const unsigned char* ac
 }
 
 // half h of a K-step's MFMAs: output channel tiles n = 2h, 2h+1
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>), in order
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (N > 0) {
+        static_for<N - 1>(f);
+        f(std::integral_constant<int, N - 1>{});
+    }
+}
+
 template <int DT, int NT>
 __device__ __forceinline__ void mfma_half(f32x4_t (&acc)[NT][4], const Frags<NT>& f, int h) {
 #pragma unroll
@@ -568,7 +577,8 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
         // GB = waves 4-7 (the SIMD partners of waves 0-3) with OAMD_STAGGER: half
         // of cur's MFMAs go before the barrier, so while waves 0-3 issue the
         // post-barrier DMA and reads, their partners keep the MFMA pipe busy
-        auto step = [&](auto NEW, auto GB, const Frags<kNT>& cur, Frags<kNT>& nxt, int i1) {
+        // xoff: uniform byte offset of the next K-step's activation rows/channels
+        auto step = [&](auto NEW, auto GB, const Frags<kNT>& cur, Frags<kNT>& nxt, int xoff) {
             constexpr bool open = decltype(NEW)::value;
             constexpr bool gb = decltype(GB)::value;
 #if OAMD_FENCE
@@ -588,7 +598,7 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
             // activation fragments do not depend on the stage barrier (the
             // layer's input is fixed): with OAMD_XEARLY they are issued before
             // it, so their latency overlaps the barrier wait
-            if constexpr (OAMD_XEARLY) load_xfrags<ABL>(nxt, act, kstep_offset<C>(i1, first), rd);
+            if constexpr (OAMD_XEARLY) load_xfrags<ABL>(nxt, act, xoff, rd);
             int sp = 0;
             if constexpr (open) {
                 // open stage g+1: it has landed (this wave's DMAs, then everyone's
@@ -605,7 +615,7 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
             }
             constexpr int kis = open ? 0 : 1;  // K-step within its stage
             load_wfrags<ABL>(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
-            if constexpr (!OAMD_XEARLY) load_xfrags<ABL>(nxt, act, kstep_offset<C>(i1, first), rd);
+            if constexpr (!OAMD_XEARLY) load_xfrags<ABL>(nxt, act, xoff, rd);
             if constexpr (open && !(ABL & 8) && OAMD_DMA_LATE)
                 issue_stage_dma<G>(wsrc, ring, g + G::RING - 2, sp, total, tid);
             if constexpr (gb) {
@@ -628,16 +638,41 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
         using NewOdd = std::integral_constant<bool, G::KS == 1>;  // K-step i1 odd
         using NewEven = std::integral_constant<bool, true>;       // K-step i1 even
         auto kloop = [&](auto GB) {
-            int i = 0;
-            for (; i + 2 < nk; i += 2) {
-                step(NewOdd{}, GB, fa, fb, i + 1);
-                step(NewEven{}, GB, fb, fa, i + 2);
-            }
-            if constexpr (nk % 2 == 0) {
-                step(NewOdd{}, GB, fa, fb, nk - 1);
-                mfma_frags<DT>(acc, fb);
+            if constexpr (first) {
+                int i = 0;
+                for (; i + 2 < nk; i += 2) {
+                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(i + 1, true));
+                    step(NewEven{}, GB, fb, fa, kstep_offset<C>(i + 2, true));
+                }
+                if constexpr (nk % 2 == 0) {
+                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(nk - 1, true));
+                    mfma_frags<DT>(acc, fb);
+                } else {
+                    mfma_frags<DT>(acc, fa);
+                }
             } else {
-                mfma_frags<DT>(acc, fa);
+                // tower conv, unrolled by tap: KPT K-steps (channel blocks c) per
+                // tap; the tap's row offset is computed once, the channel block
+                // is an immediate on the fragment reads. K-step (t, c) is current,
+                // the step loads (t, c + 1) or (t + 1, 0).
+                constexpr int KPT = C / 32;
+                static_assert(KPT % 2 == 0, "ping-pong parity per tap");
+                auto tapoff = [](int t) { return ((t / 3 - 1) * 10 + (t - 3 * (t / 3) - 1)) * G::RP; };
+                auto tap_steps = [&](int t, auto LAST) {
+                    constexpr bool last = decltype(LAST)::value;
+                    const int to = tapoff(t), tn = last ? 0 : tapoff(t + 1);
+                    static_for<last ? KPT - 1 : KPT>([&](auto J) {
+                        constexpr int c = decltype(J)::value;
+                        // the loaded K-step t*KPT + c + 1 opens a stage when it is even
+                        using NEW = std::integral_constant<bool, G::KS == 1 || (c + 1) % 2 == 0>;
+                        const int xoff = c + 1 == KPT ? tn : to + (c + 1) * 64;
+                        if constexpr (c % 2 == 0) step(NEW{}, GB, fa, fb, xoff);
+                        else step(NEW{}, GB, fb, fa, xoff);
+                    });
+                };
+                for (int t = 0; t < 8; ++t) tap_steps(t, std::false_type{});
+                tap_steps(8, std::true_type{});
+                mfma_frags<DT>(acc, fb);  // K-step 9*KPT - 1 (odd c)
             }
         };
         if (OAMD_STAGGER && wave >= 4) {
