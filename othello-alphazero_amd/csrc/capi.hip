@@ -18,6 +18,13 @@
 using namespace oamd;
 
 constexpr int kMaxPipeline = 4;
+// NN launches of the pipeline groups run one after another (a token event), so
+// each owns every CU while the other groups' tree kernels run beside it and
+// its HIP-event duration is its own (OAMD_NN_TOKEN=0: A/B builds only)
+#ifndef OAMD_NN_TOKEN
+#define OAMD_NN_TOKEN 1
+#endif
+constexpr bool kNnToken = OAMD_NN_TOKEN;
 
 namespace {
 
@@ -774,12 +781,12 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             // NN launches of the groups run one after another (a token event):
             // each owns all CUs' MFMA pipes while the other groups' tree
             // kernels run beside it
-            if (K > 1 && (s > 0 || k > 0)) HIPCHK(hipStreamWaitEvent(st[k], e->nn_token, 0));
+            if (K > 1 && kNnToken && (s > 0 || k > 0)) HIPCHK(hipStreamWaitEvent(st[k], e->nn_token, 0));
             if (ev) HIPCHK(hipEventRecord(ev[2], st[k]));
             launch_resnet_packed(N, E.feat + r0 * E.FW, E.FW, E.H, ng[k] * L, E.policy + r0 * 65, E.value + r0,
                                  st[k]);
             if (ev) HIPCHK(hipEventRecord(ev[3], st[k]));
-            if (K > 1) HIPCHK(hipEventRecord(e->nn_token, st[k]));
+            if (K > 1 && kNnToken) HIPCHK(hipEventRecord(e->nn_token, st[k]));
             launch_backup(E, st[k], g0[k], ng[k]);
             if (ev) HIPCHK(hipEventRecord(ev[4], st[k]));
         }

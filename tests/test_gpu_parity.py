@@ -223,6 +223,12 @@ def test_gpu_mcts_matches_oracle_two_threads_noise(om):
     _play_vs_oracle(om, 6, history_size=8, num_threads=2, batch_size=16, dirichlet_epsilon=0.25)
 
 
+def test_gpu_mcts_matches_oracle_many_leaves_per_step(om):
+    # L = 3 x 48 = 144 leaves per step: k_backup's per-chunk prefetch runs over
+    # chunks of 64, 64 and 16 leaves; duplicates within a step are frequent
+    _play_vs_oracle(om, 4, history_size=8, num_threads=3, batch_size=48, dirichlet_epsilon=0.25)
+
+
 def test_gpu_mcts_matches_oracle_endgame_passes(om):
     """Deep into random games (terminal leaves, passes, tree reuse over many moves)."""
     m = _mcts(om, history_size=3, num_simulations=96, num_threads=2, batch_size=8, dirichlet_epsilon=0.25)
