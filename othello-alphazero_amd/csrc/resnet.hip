@@ -162,8 +162,10 @@ constexpr TilePos make_tile_pos() {
 __constant__ TilePos kTilePos = make_tile_pos();
 
 // Workgroup geometry: C channels, BOARDS boards per workgroup, WC output
-// channels per wave (NT = WC/16 MFMA tiles), at most RING_MAX weight slots.
-template <int C_, int BOARDS_, int WC_, int RING_MAX_>
+// channels per wave (NT = WC/16 MFMA tiles), at most RING_MAX weight slots of
+// STAGE bytes (a whole number of K-steps; the packed weights are K-step
+// granular, so any stage size reads the same buffer).
+template <int C_, int BOARDS_, int WC_, int RING_MAX_, int STAGE_ = stage_bytes<C_>()>
 struct GeoT {
     static constexpr int C = C_;
     static constexpr int BOARDS = BOARDS_;
@@ -175,9 +177,9 @@ struct GeoT {
     static constexpr int RP = 2 * C + 16;       // row pitch (bytes)
     static constexpr int BROWS = 100;           // 10x10 padded board
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
-    static constexpr int KS = ksteps_per_stage(C);
     static constexpr int KSTEP_BYTES = 32 * C * 2;
-    static constexpr int STAGE = stage_bytes<C>();
+    static constexpr int STAGE = STAGE_;
+    static constexpr int KS = STAGE / KSTEP_BYTES;
     static constexpr int DPT = STAGE / 16 / THREADS;         // DMAs per thread per stage
     static constexpr int RING_FIT = (kLdsBytes - ACT_BYTES) / STAGE;
     static constexpr int RING = RING_FIT < RING_MAX_ ? RING_FIT : RING_MAX_;  // weight ring slots
@@ -187,6 +189,7 @@ struct GeoT {
     static constexpr int VM_OPEN = (RING - 3) * DPT;   // vmcnt at a stage-opening barrier
     static constexpr int VM_LAYER = (RING - 2) * DPT;  // vmcnt after an epilogue's extra issue
     static_assert(RING >= 3 && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
+    static_assert(ksteps_first(C) % KS == 0 && ksteps_tower(C) % KS == 0, "whole stages per layer");
     static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 63, "decomposition");
 };
 // throughput geometry: 512 positions x C channels per workgroup, 8 waves
@@ -201,6 +204,11 @@ using Geo = GeoT<C, 512 / C, OAMD_WC, 3>;
 #endif
 template <int C>
 using GeoS = GeoT<C, 1, C / 4, OAMD_SMALL_RING>;
+// two workgroups per CU (C=128): 2 boards and 8 KiB stages per workgroup
+// (79 KB of LDS), so one workgroup's barriers and epilogues can overlap the
+// other's MFMAs, at twice the weight streaming per FLOP
+template <int C>
+using Geo2 = GeoT<C, 2, 64, 3, 8192>;
 
 template <int DT>
 __device__ __forceinline__ uint32_t to_act(float v) {
@@ -740,6 +748,9 @@ static int ablation() {
 }
 #endif
 
+#ifndef OAMD_TWO_PER_CU
+#define OAMD_TWO_PER_CU 0
+#endif
 #ifndef OAMD_SMALL_BATCH_ROWS
 #define OAMD_SMALL_BATCH_ROWS 1024
 #endif
@@ -775,8 +786,13 @@ static void dispatch(const NetView& N, const void* feat, int fw, int H, int rows
             if (N.dtype == OAMD_FP16) launch_t<GeoS<128>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
             else launch_t<GeoS<128>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
         } else {
+#if OAMD_TWO_PER_CU
+            if (N.dtype == OAMD_FP16) launch_t<Geo2<128>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
+            else launch_t<Geo2<128>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+#else
             if (N.dtype == OAMD_FP16) launch_t<Geo<128>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
             else launch_t<Geo<128>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+#endif
         }
     } else {
         if (small) {
