@@ -63,7 +63,8 @@ constexpr int kLdsBytes = 160 * 1024;
 // forcing reads before MFMAs (OAMD_READS_FIRST), placing the DMA between MFMAs
 // (OAMD_DMA_LATE) and s_setprio around MFMA runs (OAMD_PRIO) each lose 1-4 %;
 // issuing the activation fragments before the stage barrier (OAMD_XEARLY)
-// gains 3.6 %; 128-channel wave tiles (OAMD_WC=128, one wave per SIMD) lose 3 %.
+// gains 3.6 %; 128-channel wave tiles (OAMD_WC=128, one wave per SIMD) lose 3 %;
+// a fine interleave, one fragment read then 4 MFMAs (OAMD_ILV=1), gains 2.5 %.
 #ifndef OAMD_STAGE128
 #define OAMD_STAGE128 16384
 #endif
@@ -81,6 +82,9 @@ constexpr int kLdsBytes = 160 * 1024;
 #endif
 #ifndef OAMD_XEARLY
 #define OAMD_XEARLY 1
+#endif
+#ifndef OAMD_ILV
+#define OAMD_ILV 1
 #endif
 #ifndef OAMD_STAGGER
 #define OAMD_STAGGER 0
@@ -640,6 +644,32 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
                 __builtin_amdgcn_sched_group_barrier(0x008, gb ? 4 : 12, 0);
             } else {
                 __builtin_amdgcn_sched_group_barrier(0x008, gb ? 8 : 16, 0);
+            }
+#endif
+#if OAMD_ILV
+            // fine interleave of the step's fragment reads with its 16 MFMAs: a
+            // stage-opening step has the 4 weight reads after the barrier (the
+            // activation reads precede it, OAMD_XEARLY), the other step all 8
+            if constexpr (!gb) {
+                constexpr int nds = open && OAMD_XEARLY ? 4 : 8;
+                if constexpr (OAMD_ILV == 2 && open) __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
+                if constexpr (OAMD_ILV == 5 && open) {  // DMA after the first read + 4 MFMAs
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 16 / nds, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
+                }
+                static_for<(OAMD_ILV == 4 ? nds / 2 : (OAMD_ILV == 5 && open ? nds - 1 : nds))>([&](auto) {
+                    if constexpr (OAMD_ILV == 4) {
+                        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 32 / nds, 0);
+                    } else if constexpr (OAMD_ILV == 3) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 16 / nds, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    } else {
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 16 / nds, 0);
+                    }
+                });
             }
 #endif
         };
