@@ -457,6 +457,7 @@ __device__ __forceinline__ void load_bias(float4 (&bv)[G::NT], const NetView& N,
 
 // ABL != 0 only in diagnostic ablation builds (OAMD_RESNET_ABLATE, wrong results):
 // bit 0 = no in-loop barrier/DMA wait, 1 = no activation fragment reads,
+// 16 = no epilogue stores (accumulators keep running into the next layer),
 // 2 = no weight fragment reads, 3 = no in-loop weight DMA
 template <class G, int DT, int IN, int ABL = 0>
 __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __restrict__ feat_in,
@@ -730,6 +731,7 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
         for (int n = 0; n < kNT; ++n)
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
+                if constexpr (ABL & 16) continue;
                 u32x2_t* p = reinterpret_cast<u32x2_t*>(act + wr[m] + n * 32);
                 if constexpr (kind == 1) skip[n][m] = *p;  // block input, needed by conv2
                 const f32x4_t a = acc[n][m];
@@ -801,6 +803,7 @@ static void dispatch(const NetView& N, const void* feat, int fw, int H, int rows
                 case 8: return launch_t<Geo<128>, OAMD_BF16, IN, 8>(N, feat, fw, H, rows, pol, val, s);
                 case 9: return launch_t<Geo<128>, OAMD_BF16, IN, 9>(N, feat, fw, H, rows, pol, val, s);
                 case 15: return launch_t<Geo<128>, OAMD_BF16, IN, 15>(N, feat, fw, H, rows, pol, val, s);
+                case 16: return launch_t<Geo<128>, OAMD_BF16, IN, 16>(N, feat, fw, H, rows, pol, val, s);
                 default: break;
             }
         }
