@@ -86,6 +86,10 @@ constexpr int kLdsBytes = 160 * 1024;
 #ifndef OAMD_ILV
 #define OAMD_ILV 1
 #endif
+#ifndef OAMD_DEEP_DMA
+#define OAMD_DEEP_DMA 1
+#endif
+static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the per-step lgkmcnt(0) fence");
 #ifndef OAMD_STAGGER
 #define OAMD_STAGGER 0
 #endif
@@ -188,10 +192,13 @@ struct GeoT {
     static constexpr int RING_FIT = (kLdsBytes - ACT_BYTES) / STAGE;
     static constexpr int RING = RING_FIT < RING_MAX_ ? RING_FIT : RING_MAX_;  // weight ring slots
     static constexpr int LDS = ACT_BYTES + RING * STAGE;
-    // The slot of stage s + RING - 2 is issued at the barrier that opens stage s,
-    // so RING - 2 stages are in flight while one is read.
-    static constexpr int VM_OPEN = (RING - 3) * DPT;   // vmcnt at a stage-opening barrier
-    static constexpr int VM_LAYER = (RING - 2) * DPT;  // vmcnt after an epilogue's extra issue
+    // The barrier that opens stage s issues stage s + AHEAD. Every wave has
+    // retired its reads of stage s-1 before that barrier (the per-step
+    // lgkmcnt(0) fence), so s-1's slot is free and AHEAD = RING - 1 stages fly
+    // while one is read (OAMD_DEEP_DMA=0: RING - 2, no reliance on the fence).
+    static constexpr int AHEAD = OAMD_DEEP_DMA ? RING - 1 : RING - 2;
+    static constexpr int VM_OPEN = (AHEAD - 1) * DPT;  // vmcnt at a stage-opening barrier
+    static constexpr int VM_LAYER = AHEAD * DPT;       // vmcnt after an epilogue's extra issue
     static_assert(RING >= 3 && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
     static_assert(ksteps_first(C) % KS == 0 && ksteps_tower(C) % KS == 0, "whole stages per layer");
     static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 63, "decomposition");
@@ -482,7 +489,7 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
 
     // weight stream starts right away: stages 0 .. RING-2
 #pragma unroll
-    for (int s = 0; s + 1 < G::RING; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
+    for (int s = 0; s <= G::AHEAD; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
 
     float4 bv[kNT];  // folded bias of this lane's output channels (current layer)
     load_bias<G>(bv, N, 0, wn, lane);
@@ -620,9 +627,9 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
                     wait_vm<G::VM_OPEN>();
                     __builtin_amdgcn_s_barrier();
                 }
-                sp = slot == 0 ? G::RING - 1 : slot - 1;  // (g + RING - 1) % RING
+                sp = (slot + G::AHEAD + 1) % G::RING;  // (g + 1 + AHEAD) % RING
                 if constexpr (!(ABL & 8) && !OAMD_DMA_LATE)
-                    issue_stage_dma<G>(wsrc, ring, g + G::RING - 1, sp, total, tid);
+                    issue_stage_dma<G>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
                 ++g;
                 slot = slot == G::RING - 1 ? 0 : slot + 1;
             }
@@ -630,7 +637,7 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
             load_wfrags<ABL>(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
             if constexpr (!OAMD_XEARLY) load_xfrags<ABL>(nxt, act, xoff, rd);
             if constexpr (open && !(ABL & 8) && OAMD_DMA_LATE)
-                issue_stage_dma<G>(wsrc, ring, g + G::RING - 2, sp, total, tid);
+                issue_stage_dma<G>(wsrc, ring, g + G::AHEAD, sp, total, tid);
             if constexpr (gb) {
                 mfma_half<DT>(acc, cur, 1);
             } else {
@@ -726,7 +733,7 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
         const bool more = layer + 1 < nlayers;
         if (more) load_bias<G>(bv, N, layer + 1, wn, lane);
         lds_barrier();  // every wave is done reading this layer's input and stage g
-        issue_stage_dma<G>(wsrc, ring, g + G::RING - 1, slot == 0 ? G::RING - 1 : slot - 1, total, tid);
+        issue_stage_dma<G>(wsrc, ring, g + 1 + G::AHEAD, (slot + G::AHEAD + 1) % G::RING, total, tid);
 #pragma unroll
         for (int n = 0; n < kNT; ++n)
 #pragma unroll
