@@ -229,6 +229,18 @@ def test_gpu_mcts_matches_oracle_many_leaves_per_step(om):
     _play_vs_oracle(om, 4, history_size=8, num_threads=3, batch_size=48, dirichlet_epsilon=0.25)
 
 
+def test_gpu_mcts_matches_oracle_max_history(om):
+    # history_size = 15: 31 input planes, the widest packed feature row
+    _play_vs_oracle(om, 3, history_size=15, num_simulations=256, num_threads=2, batch_size=16,
+                    dirichlet_epsilon=0.25)
+
+
+def test_gpu_mcts_matches_oracle_max_leaves_per_step(om):
+    # num_threads * batch_size = 1024 (the engine's limit): one step per search,
+    # 16 backup chunks of 64 leaves, most leaves duplicates of few nodes
+    _play_vs_oracle(om, 2, history_size=4, num_simulations=1024, num_threads=4, batch_size=256)
+
+
 def test_gpu_mcts_matches_oracle_endgame_passes(om):
     """Deep into random games (terminal leaves, passes, tree reuse over many moves)."""
     m = _mcts(om, history_size=3, num_simulations=96, num_threads=2, batch_size=8, dirichlet_epsilon=0.25)

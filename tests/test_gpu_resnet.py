@@ -73,6 +73,24 @@ def test_native_net_vs_torch_fp32_restatement(om, rows, dtype):
     torch.testing.assert_close(out["policy"].sum(1), torch.ones(rows, device=DEV), atol=1e-5, rtol=0)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_native_net_max_history_vs_restatement(om, dtype):
+    """31 input planes (history 15) through the packed-row and fp32 paths."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    sd = alphazero_state_dict(5, 31, 128, 2, 64)
+    net = om.NativeNet(sd, device=0, dtype=dtype)
+    gen = torch.Generator().manual_seed(31)
+    x = (torch.rand((300, 31, 8, 8), generator=gen) < 0.3).float()
+    x[:, 0] = (torch.rand((300, 1, 1), generator=gen) < 0.5).float()
+    x = x.to(DEV)
+    ref = resnet_ref.forward(sd, x)
+    out = net(x)
+    tp, tv = TOL[dtype]
+    assert (out["policy"] - ref["policy"]).abs().max().item() <= tp
+    assert (out["value"] - ref["value"]).abs().max().item() <= tv
+
+
 def test_native_search_equals_callback_search(om):
     """The packed-feature native path and the fp32-feature callback path feed the
     same kernel the same planes: visit counts must agree exactly."""
