@@ -55,6 +55,11 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 #ifndef OAMD_WC
 #define OAMD_WC 64
 #endif
+// C=256 (2 boards per workgroup, one K-step per 16 KiB stage): 128-channel wave
+// tiles halve the barriers per MFMA and measure 7.8 % faster than 64 (same box)
+#ifndef OAMD_WC256
+#define OAMD_WC256 128
+#endif
 constexpr int kLdsBytes = 160 * 1024;
 // Weight stage = 16 KiB (2 K-steps at C=128, 1 at C=256) in a 3-slot ring.
 // Compile-time schedule knobs, A/B-measured on MI355X with tools/ab.sh (same box,
@@ -88,6 +93,11 @@ constexpr int kLdsBytes = 160 * 1024;
 #endif
 #ifndef OAMD_DEEP_DMA
 #define OAMD_DEEP_DMA 1
+#endif
+// weight stream by register staging (global_load_dwordx4 -> VGPRs -> ds_write_b128
+// one stage later) instead of LDS-DMA, in a 2-slot ring
+#ifndef OAMD_REGSTAGE
+#define OAMD_REGSTAGE 0
 #endif
 static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the per-step lgkmcnt(0) fence");
 #ifndef OAMD_STAGGER
@@ -199,13 +209,13 @@ struct GeoT {
     static constexpr int AHEAD = OAMD_DEEP_DMA ? RING - 1 : RING - 2;
     static constexpr int VM_OPEN = (AHEAD - 1) * DPT;  // vmcnt at a stage-opening barrier
     static constexpr int VM_LAYER = AHEAD * DPT;       // vmcnt after an epilogue's extra issue
-    static_assert(RING >= 3 && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
+    static_assert(RING >= (OAMD_REGSTAGE ? 2 : 3) && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
     static_assert(ksteps_first(C) % KS == 0 && ksteps_tower(C) % KS == 0, "whole stages per layer");
     static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 63, "decomposition");
 };
 // throughput geometry: 512 positions x C channels per workgroup, 8 waves
 template <int C>
-using Geo = GeoT<C, 512 / C, OAMD_WC, 3>;
+using Geo = GeoT<C, 512 / C, C == 256 ? OAMD_WC256 : OAMD_WC, OAMD_REGSTAGE ? 2 : 3>;
 // small-batch geometry (latency): one board per workgroup, 4 waves of C/4
 // channels, so a handful of rows spreads over as many CUs as boards; the LDS
 // ring depth (4, 6 or 8 slots) measured equal: at 8 MFMAs per wave and K-step
@@ -214,7 +224,7 @@ using Geo = GeoT<C, 512 / C, OAMD_WC, 3>;
 #define OAMD_SMALL_RING 4
 #endif
 template <int C>
-using GeoS = GeoT<C, 1, C / 4, OAMD_SMALL_RING>;
+using GeoS = GeoT<C, 1, C / 4, OAMD_REGSTAGE ? 2 : OAMD_SMALL_RING>;
 // two workgroups per CU (C=128): 2 boards and 8 KiB stages per workgroup
 // (79 KB of LDS), so one workgroup's barriers and epilogues can overlap the
 // other's MFMAs, at twice the weight streaming per FLOP
@@ -357,6 +367,23 @@ __device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsig
     }
 }
 
+// register-staged weight stream: this thread's 16-byte chunks of stage g
+// (same linear chunk -> LDS mapping as the LDS-DMA path)
+template <class G>
+__device__ __forceinline__ void stage_load_regs(u32x4_t (&stg)[G::DPT], const unsigned char* wsrc, int g, int total,
+                                                int tid) {
+    const unsigned char* src = wsrc + (size_t)(g < total ? g : total - 1) * G::STAGE;
+#pragma unroll
+    for (int i = 0; i < G::DPT; ++i)
+        stg[i] = *reinterpret_cast<const u32x4_t*>(src + (size_t)(i * G::THREADS + tid) * 16);
+}
+template <class G>
+__device__ __forceinline__ void stage_store_lds(const u32x4_t (&stg)[G::DPT], unsigned char* ring, int slot, int tid) {
+    unsigned char* dst = ring + slot * G::STAGE;
+#pragma unroll
+    for (int i = 0; i < G::DPT; ++i) *reinterpret_cast<u32x4_t*>(dst + (i * G::THREADS + tid) * 16) = stg[i];
+}
+
 // s_waitcnt vmcnt(N): all but this wave's N youngest LDS-DMA / global ops done
 // (gfx9 encoding: vmcnt[3:0], expcnt[6:4] = 7, lgkmcnt[11:8] = 15: no wait on those)
 template <int N>
@@ -487,9 +514,19 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
     const int total = (ksteps_first(C) + 2 * N.R * ksteps_tower(C)) / G::KS;
 
-    // weight stream starts right away: stages 0 .. RING-2
+    // weight stream starts right away: stages 0 .. AHEAD (register staging:
+    // stages 0 and 1 go to LDS now, stage 2 waits in VGPRs)
+    u32x4_t stg[G::DPT];
+    if constexpr (OAMD_REGSTAGE) {
+        stage_load_regs<G>(stg, wsrc, 0, total, tid);
+        stage_store_lds<G>(stg, ring, 0, tid);
+        stage_load_regs<G>(stg, wsrc, 1, total, tid);
+        stage_store_lds<G>(stg, ring, 1 % G::RING, tid);
+        stage_load_regs<G>(stg, wsrc, 2, total, tid);
+    } else {
 #pragma unroll
-    for (int s = 0; s <= G::AHEAD; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
+        for (int s = 0; s <= G::AHEAD; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
+    }
 
     float4 bv[kNT];  // folded bias of this lane's output channels (current layer)
     load_bias<G>(bv, N, 0, wn, lane);
@@ -563,7 +600,7 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
     int slot = 0;  // g % RING
 
     // stage 0 and the input planes must be visible (bias loads are older than the DMAs)
-    wait_vm<G::VM_LAYER>();
+    if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();
     lds_barrier();
     load_frags(fa, act, ring, kstep_offset<C>(0, true), rd, wl);
 
@@ -624,12 +661,17 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
                 // open stage g+1: it has landed (this wave's DMAs, then everyone's
                 // via the barrier) and stage g-1's slot is drained by all waves
                 if constexpr (!(ABL & 1)) {
-                    wait_vm<G::VM_OPEN>();
+                    if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_OPEN>();
                     __builtin_amdgcn_s_barrier();
                 }
                 sp = (slot + G::AHEAD + 1) % G::RING;  // (g + 1 + AHEAD) % RING
-                if constexpr (!(ABL & 8) && !OAMD_DMA_LATE)
+                if constexpr (OAMD_REGSTAGE) {
+                    // stage g+2 into the slot stage g just left; fetch stage g+3
+                    stage_store_lds<G>(stg, ring, (slot + 2) % G::RING, tid);
+                    stage_load_regs<G>(stg, wsrc, g + 3, total, tid);
+                } else if constexpr (!(ABL & 8) && !OAMD_DMA_LATE) {
                     issue_stage_dma<G>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
+                }
                 ++g;
                 slot = slot == G::RING - 1 ? 0 : slot + 1;
             }
@@ -733,7 +775,12 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
         const bool more = layer + 1 < nlayers;
         if (more) load_bias<G>(bv, N, layer + 1, wn, lane);
         lds_barrier();  // every wave is done reading this layer's input and stage g
-        issue_stage_dma<G>(wsrc, ring, g + 1 + G::AHEAD, (slot + G::AHEAD + 1) % G::RING, total, tid);
+        if constexpr (OAMD_REGSTAGE) {
+            stage_store_lds<G>(stg, ring, (slot + 2) % G::RING, tid);
+            stage_load_regs<G>(stg, wsrc, g + 3, total, tid);
+        } else {
+            issue_stage_dma<G>(wsrc, ring, g + 1 + G::AHEAD, (slot + G::AHEAD + 1) % G::RING, total, tid);
+        }
 #pragma unroll
         for (int n = 0; n < kNT; ++n)
 #pragma unroll
@@ -747,7 +794,7 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
         ++g;
         slot = slot == G::RING - 1 ? 0 : slot + 1;
         if (more) {
-            wait_vm<G::VM_LAYER>();  // stage g has landed (later stages may still fly)
+            if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();  // stage g has landed (later may fly)
             lds_barrier();           // ... and this layer's output is complete
             load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false), rd, wl);
         }

@@ -15,7 +15,10 @@ from othello_mcts.synthetic import alphazero_state_dict  # noqa: E402
 
 rows = int(os.environ.get("ROWS", "8192"))
 v = os.environ.get("OAMD_RESNET_ABLATE", "0")
-net = om.NativeNet(alphazero_state_dict(1, 17, 128, 9, 128), device=0)
+C = int(os.environ.get("NN_C", "128"))  # 128 -> 128x10b, 256 -> 256x20b
+R = 9 if C == 128 else 19
+net = om.NativeNet(alphazero_state_dict(1, 17, C, R, C), device=0)
+flops = 2.0 * 64 * 9 * C * (17 + 2 * R * C) + 2.0 * (64 * C * 3 + 128 * 65 + 64 * C + C)  # bench.py
 x = (torch.rand((rows, 17, 8, 8), device="cuda") < 0.3).float()
 for _ in range(3):
     net(x)
@@ -31,4 +34,4 @@ for _ in range(5):
     ms.append(a.elapsed_time(b) / 10)
 ms.sort()
 t = ms[len(ms) // 2]
-print(f"variant {v}: {t:.3f} ms/launch  {342327808.0 * rows / t / 1e9:.1f} TFLOP/s  (rows={rows})", flush=True)
+print(f"variant {v}: {t:.3f} ms/launch  {flops * rows / t / 1e9:.1f} TFLOP/s  (rows={rows})", flush=True)
