@@ -142,9 +142,17 @@ def main() -> None:
     args = ap.parse_args()
 
     world, rank, local = dist_env()
+    # OAMD_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
+    # devices round-robin, timing reduced over gloo); the driver's runs use RCCL
+    backend = os.environ.get("OAMD_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import othello_mcts as om
     from othello_mcts.synthetic import alphazero_state_dict
@@ -174,7 +182,7 @@ def main() -> None:
         for _ in range(args.steps):
             step()
 
-    dt_max = timed_max(world, run, torch.cuda.synchronize, "cuda")
+    dt_max = timed_max(world, run, torch.cuda.synchronize, "cpu" if backend == "gloo" else "cuda")
     ms1, launches1, rows1 = b.engine.nn_timing()
     sel1, bk1, _ = b.engine.tree_timing()
     value = aggregate_rate(world, args.games, sims_per_search, args.steps, dt_max)
