@@ -139,6 +139,7 @@ def main() -> None:
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=2025)
+    ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -168,7 +169,7 @@ def main() -> None:
     sims_per_search = L * ((args.sims + L - 1) // L)
 
     def step():
-        b.search(net)
+        b.search(net, sync=args.sync_search)  # enqueue only; the timed region syncs at its end
         b.selfplay_move(temperature_moves=12, opening_moves=8, emit_targets=True)
 
     for _ in range(args.warmup):

@@ -151,7 +151,8 @@ int oamd_engine_reset(oamd_engine *e, int32_t game, uint64_t seed);
 /* Whole search for every active game with the native net
  * (MCTS::search, mcts.h:220-256). Outputs are optional (may be NULL):
  * simulations = leaf selections (sum over games), evaluations = NN rows of
- * non-terminal leaves. */
+ * non-terminal leaves. With both NULL the call returns once the search is
+ * enqueued (stream order; the host does not wait), otherwise after it ends. */
 int oamd_engine_search(oamd_engine *e, oamd_net *net, int64_t *simulations, int64_t *evaluations);
 /* Split the games into `groups` pipeline groups (own HIP streams) so that tree
  * kernels of one group overlap the NN launch of another (0 = auto: 2 groups
@@ -227,11 +228,12 @@ int oamd_engine_random_openings(oamd_engine *e, int32_t max_moves, uint64_t seed
 /* The random-stream key of a game (DESIGN.md "Random streams"). */
 int oamd_engine_game_key(oamd_engine *e, int32_t game, uint64_t *key_host);
 
-/* Timing of the last oamd_engine_search (HIP events on the engine stream):
+/* Timing accumulated over the timed oamd_engine_search calls (HIP events on
+ * the launching streams; a query waits for the searches still in flight):
  * total ms spent in the NN kernel, number of NN launches, rows evaluated. */
 int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches, int64_t *rows);
 /* Same for the tree kernels: total ms in k_select and in k_backup (one launch
- * of each per NN launch). Timed searches record 5 HIP events per step and
+ * of each per NN launch). Timed searches record 6 HIP events per step and
  * pipeline group on the group's stream. */
 int oamd_engine_tree_timing(const oamd_engine *e, float *select_ms, float *backup_ms, int64_t *launches);
 int oamd_engine_enable_timing(oamd_engine *e, int32_t enable);

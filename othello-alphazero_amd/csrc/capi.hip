@@ -18,13 +18,17 @@
 using namespace oamd;
 
 constexpr int kMaxPipeline = 4;
-// NN launches of the pipeline groups run one after another (a token event), so
-// each owns every CU while the other groups' tree kernels run beside it and
-// its HIP-event duration is its own (OAMD_NN_TOKEN=0: A/B builds only)
-#ifndef OAMD_NN_TOKEN
-#define OAMD_NN_TOKEN 1
+constexpr int kEvPerBlock = 6;  // timing events per (step, group)
+// NN launches of the pipeline groups run one after another, so each owns every
+// CU while the other groups' tree kernels run beside it and its HIP-event
+// duration is its own. OAMD_NN_ORDER 1: a token event passed between the group
+// streams; 2: all NN launches on one NN stream (a group's launch waits for its
+// select, its backup for the launch); 0: unordered (A/B only). Kernel traces
+// show the same gap between consecutive launches for 1 and 2 (~14 us, ~24 us
+// with the timing events), and 1 measured 0.4 % faster in the bench.
+#ifndef OAMD_NN_ORDER
+#define OAMD_NN_ORDER 1
 #endif
-constexpr bool kNnToken = OAMD_NN_TOKEN;
 
 namespace {
 
@@ -154,15 +158,47 @@ struct oamd_engine {
     hipStream_t pipe_stream[kMaxPipeline] = {};
     hipEvent_t fork_ev = nullptr;
     hipEvent_t nn_token = nullptr;
+    hipStream_t nn_stream = nullptr;
+    hipEvent_t sel_ev[kMaxPipeline] = {};
+    hipEvent_t nn_ev[kMaxPipeline] = {};
     hipEvent_t join_ev[kMaxPipeline] = {};
-    // timing
+    // timing: kEvPerBlock events per (step, group) of a search, in two pools used in
+    // turn, so a search never waits for the previous one's events; a pool is
+    // summed (waiting for its last event) before reuse or on a timing query
     bool timing = false;
-    std::vector<hipEvent_t> ev;
+    std::vector<hipEvent_t> ev[2];
+    int ev_blocks[2] = {0, 0};  // pending (step, group) blocks per pool
+    int64_t ev_rows[2] = {0, 0};
+    int ev_cur = 0;
     float nn_ms = 0.0f;
     float select_ms = 0.0f;
     float backup_ms = 0.0f;
     int64_t nn_launches = 0;
     int64_t nn_rows = 0;
+
+    int resolve_timing(int p) {
+        const int n = ev_blocks[p];
+        if (!n) return OAMD_OK;
+        HIPCHK(hipEventSynchronize(ev[p][kEvPerBlock * n - 1]));
+        for (int i = 0; i < n; ++i) {
+            const hipEvent_t* b = &ev[p][kEvPerBlock * i];
+            float ms = 0.0f;
+            HIPCHK(hipEventElapsedTime(&ms, b[0], b[1]));
+            select_ms += ms;
+            HIPCHK(hipEventElapsedTime(&ms, b[2], b[3]));
+            nn_ms += ms;
+            HIPCHK(hipEventElapsedTime(&ms, b[4], b[5]));
+            backup_ms += ms;
+        }
+        nn_launches += n;
+        nn_rows += ev_rows[p];
+        ev_blocks[p] = 0;
+        return OAMD_OK;
+    }
+    int resolve_all_timing() {
+        int rc = resolve_timing(ev_cur ^ 1);
+        return rc ? rc : resolve_timing(ev_cur);
+    }
 
     int L() const { return cfg.num_threads * cfg.batch_size; }
 
@@ -170,9 +206,13 @@ struct oamd_engine {
         if (K <= 1) return OAMD_OK;
         if (!fork_ev) HIPCHK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
         if (!nn_token) HIPCHK(hipEventCreateWithFlags(&nn_token, hipEventDisableTiming));
+        if (!nn_stream) HIPCHK(hipStreamCreateWithFlags(&nn_stream, hipStreamNonBlocking));
         while (n_pipe_streams < K) {
-            HIPCHK(hipStreamCreateWithFlags(&pipe_stream[n_pipe_streams], hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&join_ev[n_pipe_streams], hipEventDisableTiming));
+            const int k = n_pipe_streams;
+            HIPCHK(hipStreamCreateWithFlags(&pipe_stream[k], hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&join_ev[k], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&sel_ev[k], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&nn_ev[k], hipEventDisableTiming));
             ++n_pipe_streams;
         }
         return OAMD_OK;
@@ -260,13 +300,17 @@ struct oamd_engine {
         dfree(visits_dev);
         dfree(q_dev);
         dfree(spd_dev);
-        for (auto e : ev) (void)hipEventDestroy(e);
+        for (auto& pool : ev)
+            for (auto e : pool) (void)hipEventDestroy(e);
         for (int k = 0; k < n_pipe_streams; ++k) {
             (void)hipStreamDestroy(pipe_stream[k]);
             (void)hipEventDestroy(join_ev[k]);
+            (void)hipEventDestroy(sel_ev[k]);
+            (void)hipEventDestroy(nn_ev[k]);
         }
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         if (nn_token) (void)hipEventDestroy(nn_token);
+        if (nn_stream) (void)hipStreamDestroy(nn_stream);
     }
 };
 
@@ -718,14 +762,18 @@ int oamd_engine_enable_timing(oamd_engine* e, int32_t enable) {
     return OAMD_OK;
 }
 
-int oamd_engine_nn_timing(const oamd_engine* e, float* nn_ms, int64_t* launches, int64_t* rows) {
+int oamd_engine_nn_timing(const oamd_engine* ce, float* nn_ms, int64_t* launches, int64_t* rows) {
+    oamd_engine* e = const_cast<oamd_engine*>(ce);  // pending events are summed here
+    if (int rc = e->resolve_all_timing()) return rc;
     if (nn_ms) *nn_ms = e->nn_ms;
     if (launches) *launches = e->nn_launches;
     if (rows) *rows = e->nn_rows;
     return OAMD_OK;
 }
 
-int oamd_engine_tree_timing(const oamd_engine* e, float* select_ms, float* backup_ms, int64_t* launches) {
+int oamd_engine_tree_timing(const oamd_engine* ce, float* select_ms, float* backup_ms, int64_t* launches) {
+    oamd_engine* e = const_cast<oamd_engine*>(ce);
+    if (int rc = e->resolve_all_timing()) return rc;
     if (select_ms) *select_ms = e->select_ms;
     if (backup_ms) *backup_ms = e->backup_ms;
     if (launches) *launches = e->nn_launches;
@@ -752,13 +800,16 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     int rc = e->ensure_streams(K);
     if (rc) return rc;
     if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
-    // timing: per (step, group) 5 events: select begin/end, NN begin (after the
-    // token wait)/end, backup end
-    const int nev = 5 * steps * K;
-    while (e->timing && (int)e->ev.size() < nev) {
-        hipEvent_t x;
-        HIPCHK(hipEventCreate(&x));
-        e->ev.push_back(x);
+    // timing: per (step, group) kEvPerBlock events: select begin/end, NN
+    // begin/end (on the NN stream, after its waits), backup begin/end
+    const int pool = e->ev_cur;
+    if (e->timing) {
+        if ((rc = e->resolve_timing(pool))) return rc;
+        while ((int)e->ev[pool].size() < kEvPerBlock * steps * K) {
+            hipEvent_t x;
+            HIPCHK(hipEventCreate(&x));
+            e->ev[pool].push_back(x);
+        }
     }
     hipStream_t st[kMaxPipeline];
     int g0[kMaxPipeline], ng[kMaxPipeline];
@@ -774,21 +825,32 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     for (int s = 0; s < steps; ++s) {
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)g0[k] * L;
-            hipEvent_t* ev = e->timing ? &e->ev[5 * (s * K + k)] : nullptr;
+            hipEvent_t* ev = e->timing ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
             if (ev) HIPCHK(hipEventRecord(ev[0], st[k]));
             launch_select(E, st[k], g0[k], ng[k]);
             if (ev) HIPCHK(hipEventRecord(ev[1], st[k]));
-            // NN launches of the groups run one after another (a token event):
-            // each owns all CUs' MFMA pipes while the other groups' tree
-            // kernels run beside it
-            if (K > 1 && kNnToken && (s > 0 || k > 0)) HIPCHK(hipStreamWaitEvent(st[k], e->nn_token, 0));
-            if (ev) HIPCHK(hipEventRecord(ev[2], st[k]));
+            // the groups' NN launches run one after another (OAMD_NN_ORDER)
+            hipStream_t ns = st[k];
+            if (K > 1 && OAMD_NN_ORDER == 2) {
+                ns = e->nn_stream;
+                HIPCHK(hipEventRecord(e->sel_ev[k], st[k]));
+                HIPCHK(hipStreamWaitEvent(ns, e->sel_ev[k], 0));
+            } else if (K > 1 && OAMD_NN_ORDER == 1 && (s > 0 || k > 0)) {
+                HIPCHK(hipStreamWaitEvent(st[k], e->nn_token, 0));
+            }
+            if (ev) HIPCHK(hipEventRecord(ev[2], ns));
             launch_resnet_packed(N, E.feat + r0 * E.FW, E.FW, E.H, ng[k] * L, E.policy + r0 * 65, E.value + r0,
-                                 st[k]);
-            if (ev) HIPCHK(hipEventRecord(ev[3], st[k]));
-            if (K > 1 && kNnToken) HIPCHK(hipEventRecord(e->nn_token, st[k]));
-            launch_backup(E, st[k], g0[k], ng[k]);
+                                 ns);
+            if (ev) HIPCHK(hipEventRecord(ev[3], ns));
+            if (K > 1 && OAMD_NN_ORDER == 2) {
+                HIPCHK(hipEventRecord(e->nn_ev[k], ns));
+                HIPCHK(hipStreamWaitEvent(st[k], e->nn_ev[k], 0));
+            } else if (K > 1 && OAMD_NN_ORDER == 1) {
+                HIPCHK(hipEventRecord(e->nn_token, st[k]));
+            }
             if (ev) HIPCHK(hipEventRecord(ev[4], st[k]));
+            launch_backup(E, st[k], g0[k], ng[k]);
+            if (ev) HIPCHK(hipEventRecord(ev[5], st[k]));
         }
     }
     LAUNCHCHK();
@@ -798,27 +860,18 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             HIPCHK(hipStreamWaitEvent(e->stream, e->join_ev[k], 0));
         }
     }
-    if (sims || evals || e->timing) {
+    if (e->timing) {
+        e->ev_blocks[pool] = steps * K;
+        e->ev_rows[pool] = (int64_t)steps * e->G * L;
+        e->ev_cur ^= 1;
+    }
+    // without counters requested the search is left in flight (stream order)
+    if (sims || evals) {
         unsigned long long c[2] = {0, 0};
-        if (sims || evals)
-            HIPCHK(hipMemcpyAsync(c, e->counters, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipMemcpyAsync(c, e->counters, sizeof(c), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
         if (sims) *sims = (int64_t)c[0];
         if (evals) *evals = (int64_t)c[1];
-        if (e->timing) {
-            for (int i = 0; i < steps * K; ++i) {
-                const hipEvent_t* ev = &e->ev[5 * i];
-                float ms = 0.0f;
-                HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[1]));
-                e->select_ms += ms;
-                HIPCHK(hipEventElapsedTime(&ms, ev[2], ev[3]));
-                e->nn_ms += ms;
-                HIPCHK(hipEventElapsedTime(&ms, ev[3], ev[4]));
-                e->backup_ms += ms;
-            }
-            e->nn_launches += (int64_t)steps * K;
-            e->nn_rows += (int64_t)steps * e->G * L;
-        }
     }
     e->step_phase = 0;
     e->steps_left = 0;

@@ -529,12 +529,18 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
         })
         .def("set_stream", [](Engine& e, uintptr_t s) { check(oamd_engine_set_stream(e.h, (void*)s)); })
         .def("reset", [](Engine& e, int game, uint64_t seed) { check(oamd_engine_reset(e.h, game, seed)); })
-        .def("search",
-             [](Engine& e, uintptr_t net) {
-                 int64_t sims = 0, evals = 0;
-                 check(oamd_engine_search(e.h, reinterpret_cast<oamd_net*>(net), &sims, &evals));
-                 return py::make_tuple(sims, evals);
-             })
+        .def(
+            "search",
+            [](Engine& e, uintptr_t net, bool sync) -> py::object {
+                if (!sync) {  // enqueue only: no counters, the host does not wait
+                    check(oamd_engine_search(e.h, reinterpret_cast<oamd_net*>(net), nullptr, nullptr));
+                    return py::none();
+                }
+                int64_t sims = 0, evals = 0;
+                check(oamd_engine_search(e.h, reinterpret_cast<oamd_net*>(net), &sims, &evals));
+                return py::make_tuple(sims, evals);
+            },
+            py::arg("net"), py::arg("sync") = true)
         .def("search_begin",
              [](Engine& e) {
                  int32_t steps = 0;

@@ -55,12 +55,16 @@ class BatchedMCTS:
         self.engine.set_stream(s)
         return s
 
-    def search(self, neural_net) -> tuple[int, int]:
-        """Run num_simulations for every active game. Returns (simulations, nn_rows)."""
+    def search(self, neural_net, sync: bool = True):
+        """Run num_simulations for every active game. Returns (simulations, nn_rows).
+
+        With the native net and ``sync=False`` the search is only enqueued on the
+        engine's stream (returns None): a self-play loop then queues the next
+        move's kernels while the GPU still runs this one's."""
         self._stream()
         nat = resolve(neural_net, self.device.index, self.config.history_size)
         if nat is not None:
-            return self.engine.search(nat.handle)
+            return self.engine.search(nat.handle, sync)
         # external evaluator: one call per step over all G * L rows
         rows = self.rows_per_step
         feat = torch.empty((rows, self._C, 8, 8), dtype=torch.float32, device=self.device)

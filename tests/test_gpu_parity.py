@@ -330,3 +330,36 @@ def test_gpu_selfplay_driver(om):
     for g in range(G):
         info = b.root_info(g)
         assert info["overflow"] == 0
+
+
+def test_gpu_async_search_matches_sync(om):
+    """search(sync=False) only enqueues; a loop of async searches + on-device
+    moves gives the same games as the synchronous loop, and the lazily summed
+    HIP-event timing counts every launch."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(5, 9, 128, 2, 32), device=0)
+    G, moves = 96, 6
+
+    def play(sync):
+        b = om.BatchedMCTS(G, history_size=4, num_simulations=64, num_threads=2, batch_size=16, seed=9,
+                           node_capacity=1 << 17)
+        b.random_openings(6, seed=4)
+        b.engine.enable_timing(True)
+        acts = []
+        for _ in range(moves):
+            r = b.search(net, sync=sync)
+            assert (r is None) == (not sync)
+            acts.append(b.selfplay_move(temperature_moves=3, emit_targets=False)["actions"].clone())
+        ms, launches, rows = b.engine.nn_timing()
+        sel, bk, launches2 = b.engine.tree_timing()
+        steps = 64 // 32
+        assert launches == launches2 == moves * steps * 2  # 2 pipeline groups at G >= 64
+        assert rows == moves * steps * G * 32
+        assert ms > 0 and sel > 0 and bk > 0
+        return torch.stack(acts).cpu().numpy(), [b.visit_counts(g) for g in range(G)]
+
+    a_sync, v_sync = play(True)
+    a_async, v_async = play(False)
+    np.testing.assert_array_equal(a_sync, a_async)
+    assert v_sync == v_async
