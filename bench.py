@@ -137,6 +137,9 @@ def main() -> None:
     ap.add_argument("--blocks", type=int, default=10, help="conv block + residual blocks")
     ap.add_argument("--hidden", type=int, default=128)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--eval-batch", type=int, default=0,
+                    help="NN rows per launch (games split into games*L/eval_batch pipeline groups; "
+                         "0 = the engine's default of 2 groups); configs[4] uses 2048")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
@@ -166,6 +169,11 @@ def main() -> None:
                        num_threads=args.threads, batch_size=args.batch, seed=engine_seed)
     b.random_openings(8, seed=opening_seed)
     L = args.threads * args.batch
+    if args.eval_batch:
+        groups, rem = divmod(args.games * L, args.eval_batch)
+        if rem or not 1 <= groups <= 8:
+            raise SystemExit(f"--eval-batch must divide games*L = {args.games * L} into 1..8 groups")
+        b.engine.set_pipeline(groups)
     sims_per_search = L * ((args.sims + L - 1) // L)
 
     def step():
@@ -198,7 +206,10 @@ def main() -> None:
     peak = PEAK_TFLOPS[args.dtype]
     workload = (f"{args.games} concurrent self-play games per GPU, {args.sims} sims/move, "
                 f"{args.channels}x{args.blocks}b ResNet {args.dtype}, history {args.history}, "
-                f"{args.threads} threads x {args.batch} leaves per step (BASELINE configs[1])")
+                f"{args.threads} threads x {args.batch} leaves per step"
+                + (f", eval batch {args.eval_batch}" if args.eval_batch else "")
+                + (" (BASELINE configs[1])" if (args.games, args.channels, args.blocks, args.sims, args.dtype,
+                                                args.eval_batch) == (256, 128, 10, 800, "bf16", 0) else ""))
     # HBM bytes per launch from the committed PMC summary of this same workload
     traffic = None
     tfile = ROOT / "profiles" / "traffic_resnet.json"
@@ -245,7 +256,8 @@ def main() -> None:
         "baseline_ref": {"value": PUBLISHED_SIMS_PER_S, "unit": "simulations/s",
                          "hardware": "1x RTX 4090 + 24-core CPU (reference README.md:25, BASELINE.md)"},
         "dtype": args.dtype,
-        "data": "synthetic: seeded random-init 128x10b AlphaZeroNet weights, random openings (0-8 plies)",
+        "data": f"synthetic: seeded random-init {args.channels}x{args.blocks}b AlphaZeroNet weights, "
+                "random openings (0-8 plies)",
         "config": {
             "workload": workload,
             "games_per_gpu": args.games,

@@ -156,7 +156,7 @@ int oamd_engine_reset(oamd_engine *e, int32_t game, uint64_t seed);
 int oamd_engine_search(oamd_engine *e, oamd_net *net, int64_t *simulations, int64_t *evaluations);
 /* Split the games into `groups` pipeline groups (own HIP streams) so that tree
  * kernels of one group overlap the NN launch of another (0 = auto: 2 groups
- * from 64 games, else 1; at most 4). Results do not depend on it. */
+ * from 64 games, else 1; at most 8). Results do not depend on it. */
 int oamd_engine_set_pipeline(oamd_engine *e, int32_t groups);
 
 /* Step-wise search for an external evaluator (the Python NeuralNet callback

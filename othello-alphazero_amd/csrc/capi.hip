@@ -17,7 +17,7 @@
 
 using namespace oamd;
 
-constexpr int kMaxPipeline = 4;
+constexpr int kMaxPipeline = 8;
 constexpr int kEvPerBlock = 6;  // timing events per (step, group)
 // NN launches of the pipeline groups run one after another, so each owns every
 // CU while the other groups' tree kernels run beside it and its HIP-event

@@ -147,7 +147,7 @@ def test_mcts_autodetects_alphazero_module(om):
 
 
 def test_pipeline_groups_do_not_change_results(om):
-    """Splitting the games over 1, 2 or 3 stream groups is a pure scheduling
+    """Splitting the games over 1, 2, 3 or 8 stream groups is a pure scheduling
     choice: every game's statistics must be identical."""
     from othello_mcts.synthetic import alphazero_state_dict
 
@@ -155,7 +155,7 @@ def test_pipeline_groups_do_not_change_results(om):
     kw = dict(history_size=4, num_simulations=96, num_threads=2, batch_size=8, seed=9,
               node_capacity=1 << 15)
     runs = []
-    for groups in (1, 2, 3):
+    for groups in (1, 2, 3, 8):
         b = om.BatchedMCTS(12, **kw)
         b.engine.set_pipeline(groups)
         b.random_openings(5, seed=3)
@@ -164,7 +164,7 @@ def test_pipeline_groups_do_not_change_results(om):
             b.selfplay_move(temperature_moves=12, opening_moves=2)
         b.search(net)
         runs.append([(b.visit_counts(g), b.mean_action_values(g)) for g in range(12)])
-    assert runs[0] == runs[1] == runs[2]
+    assert runs[0] == runs[1] == runs[2] == runs[3]
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])

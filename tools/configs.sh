@@ -10,4 +10,5 @@ run() {  # name, args
 }
 run c2 --steps 5 --warmup 1
 run c4 --steps 2 --warmup 1 --channels 256 --blocks 20 --hidden 256 --sims 1600
-run c5 --steps 3 --warmup 1 --games 512 --dtype fp16
+run c5 --steps 3 --warmup 1 --games 512 --dtype fp16 --eval-batch 2048
+run c5_8k --steps 3 --warmup 1 --games 512 --dtype fp16
