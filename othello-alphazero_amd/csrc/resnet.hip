@@ -91,6 +91,10 @@ constexpr int kLdsBytes = 160 * 1024;
 #ifndef OAMD_ILV
 #define OAMD_ILV 1
 #endif
+// MFMAs of a step over which OAMD_ILV=1 spreads the step's fragment reads
+#ifndef OAMD_ILV_SPAN
+#define OAMD_ILV_SPAN 16
+#endif
 #ifndef OAMD_DEEP_DMA
 #define OAMD_DEEP_DMA 1
 #endif
@@ -717,9 +721,14 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     } else {
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x008, 16 / nds, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, OAMD_ILV_SPAN / nds, 0);
                     }
                 });
+                // reads spread over the first OAMD_ILV_SPAN MFMAs only: the rest
+                // of the step's MFMAs cover the last read's latency before the
+                // next step's lgkmcnt(0) fence
+                if constexpr (OAMD_ILV == 1 && OAMD_ILV_SPAN != 16)
+                    __builtin_amdgcn_sched_group_barrier(0x008, kNT * 4 - nds * (OAMD_ILV_SPAN / nds), 0);
             }
 #endif
         };
