@@ -410,8 +410,9 @@ int oamd_net_create(int32_t device, const oamd_net_desc* d, oamd_net** out) {
                     "conv_channels must be 128 or 256 for the native net, got " + std::to_string(d->conv_channels));
     if (d->num_residual_blocks < 0)
         return fail(OAMD_INVALID_ARGUMENT, "num_residual_blocks must be >= 0");
-    if (d->value_head_hidden_channels < 1)
-        return fail(OAMD_INVALID_ARGUMENT, "value_head_hidden_channels must be >= 1");
+    if (d->value_head_hidden_channels < 1 || d->value_head_hidden_channels > 1024)
+        return fail(OAMD_INVALID_ARGUMENT, "value_head_hidden_channels must be in [1, 1024] for the native net, got " +
+                                               std::to_string(d->value_head_hidden_channels));
     if (d->num_squares != 64 || d->num_actions != 65)
         return fail(OAMD_INVALID_ARGUMENT, "num_squares must be 64 and num_actions 65");
     if (d->dtype != OAMD_BF16 && d->dtype != OAMD_FP16)

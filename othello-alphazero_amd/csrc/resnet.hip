@@ -405,83 +405,171 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// Policy and value heads, all waves of the workgroup together (called by every
+// thread; barriers inside). The Linear layers run k-split with every board on
+// every lane, so a workgroup reads each head weight once (not once per board):
+//   phase 1  1x1 convs + BN + ReLU, one wave per (board, head), lane = square;
+//            results (and policy logit 64, a reduction over squares) go to
+//            `scratch`, the drained weight ring;
+//   phase 2  partial dot products over 32-input chunks, lane = output unit,
+//            one task per (chunk, 64-unit slice);
+//   phase 3  per board: chunks summed in a fixed order, softmax(65) / ReLU,
+//            Linear(hidden->1), tanh.
+// Every output's arithmetic order is independent of BOARDS / WAVES, so all
+// geometries produce identical bits.
+constexpr int kMaxValueHidden = 1024;  // scratch budget (capi.hip validates)
+template <int B>
+__host__ __device__ constexpr int head_scratch_floats(int hidden) {
+    return 128 * B + 64 * B + 4 + 4 * B * 64 + 2 * B * ((hidden + 63) / 64) * 64 + 3 * 256 + 4;
+}
+
 template <class G, int DT>
-__device__ void heads(const NetView& N, const unsigned char* act, int wave, int lane, int row0, int rows,
-                      float* __restrict__ policy, float* __restrict__ value) {
+__device__ __forceinline__ void heads(const NetView& N, const unsigned char* act, unsigned char* scratch, int wave,
+                                      int lane, int row0, int rows, float* __restrict__ policy,
+                                      float* __restrict__ value) {
     constexpr int C = G::C;
-    constexpr int BOARDS = G::BOARDS;
+    constexpr int B = G::BOARDS;
+    constexpr int NW = G::WAVES;
+    static_assert(head_scratch_floats<B>(kMaxValueHidden) * 4 <= G::RING * G::STAGE, "head scratch");
     const HeadLayout HL(C, N.hidden);
     const float* hp = N.head;
-    const int b = wave % BOARDS;
-    const int gr = row0 + b;
-    if (wave >= 2 * BOARDS || gr >= rows) return;
-    const unsigned char* arow = act + (b * G::BROWS + pad_row(lane)) * G::RP;
-    if (wave < BOARDS) {
-        // policy head: 1x1 conv (C->2) + BN + ReLU, flatten c*64+s, Linear(128->65), softmax
-        float h0 = hp[HL.pcb + 0], h1 = hp[HL.pcb + 1];
-        for (int c8 = 0; c8 < C / 8; ++c8) {
-            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
-            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    const int hid = N.hidden;
+    const int nvs = (hid + 63) / 64;  // 64-unit slices of the value hidden layer
+    float* sp = reinterpret_cast<float*>(scratch);  // [128][B] policy conv outputs (k = c*64 + square)
+    float* sv = sp + 128 * B;                       // [64][B]  value conv outputs
+    float* s64 = sv + 64 * B;                       // [B]      policy logit 64 (with bias)
+    float* pp = s64 + 4;                            // [4][B][64] policy partials
+    float* pv = pp + 4 * B * 64;                    // [2][B][nvs*64] value partials
+    float* cw = pv + 2 * B * nvs * 64;              // 1x1 conv weights: pcw [2][C], vcw [C]
+
+    // Linear weights of this wave's phase-2 task (one column of 32 inputs per
+    // lane): task t < 4 covers policy inputs 32t.., task 4 + 2q + c value
+    // units 64q.. over inputs 32c... Issued first, so their global round trip
+    // overlaps the conv-weight copy and phase 1.
+    auto task_weights = [&](int task, float (&wv)[32]) {
+        const float* w;
+        int stride;
+        if (task < 4) {
+            w = hp + HL.plw + task * 32 * 65 + lane;
+            stride = 65;
+        } else {
+            const int t = task - 4, c = t & 1, j = (t >> 1) * 64 + lane;
+            w = hp + HL.v1w + c * 32 * hid + (j < hid ? j : hid - 1);
+            stride = hid;
+        }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float x = from_act<DT>((w4[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
-                h0 += x * hp[HL.pcw + c8 * 8 + e];
-                h1 += x * hp[HL.pcw + C + c8 * 8 + e];
+        for (int k = 0; k < 32; ++k) wv[k] = w[k * stride];
+    };
+    const int ntask = 4 + 2 * nvs;
+    float wv[32];
+    if (wave < ntask) task_weights(wave, wv);
+    // the 1x1 conv weights go to LDS (one global round trip for the
+    // workgroup), so the conv loops below read them as LDS broadcasts
+    for (int i = wave * 64 + lane; i < 3 * C; i += NW * 64) cw[i] = hp[i < 2 * C ? HL.pcw + i : HL.vcw + i - 2 * C];
+    __syncthreads();
+    for (int job = wave; job < 2 * B; job += NW) {
+        const int b = job % B;
+        const unsigned char* arow = act + (b * G::BROWS + pad_row(lane)) * G::RP;
+        if (job < B) {
+            // policy: 1x1 conv (C->2) + BN + ReLU; flatten c*64+s
+            const float u0 = hp[HL.plw + lane * 65 + 64], u1 = hp[HL.plw + (64 + lane) * 65 + 64];
+            float h0 = hp[HL.pcb + 0], h1 = hp[HL.pcb + 1];
+            for (int c8 = 0; c8 < C / 8; ++c8) {
+                const u32x4_t v = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float x = from_act<DT>((w4[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
+                    h0 = __builtin_fmaf(x, cw[c8 * 8 + e], h0);
+                    h1 = __builtin_fmaf(x, cw[C + c8 * 8 + e], h1);
+                }
             }
-        }
-        h0 = fmaxf(h0, 0.0f);
-        h1 = fmaxf(h1, 0.0f);
-        const float* plw = hp + HL.plw;
-        float o = hp[HL.plb + lane];
-        float o64 = hp[HL.plb + 64];
-        for (int s = 0; s < 64; ++s) {
-            const float x0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h0), s));
-            const float x1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h1), s));
-            o += plw[s * 65 + lane] * x0 + plw[(64 + s) * 65 + lane] * x1;
-            o64 += plw[s * 65 + 64] * x0 + plw[(64 + s) * 65 + 64] * x1;
-        }
-        float m = o;
+            h0 = fmaxf(h0, 0.0f);
+            h1 = fmaxf(h1, 0.0f);
+            sp[lane * B + b] = h0;
+            sp[(64 + lane) * B + b] = h1;
+            float o64 = __builtin_fmaf(u1, h1, u0 * h0);
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-        m = fmaxf(m, o64);
-        const float e = __expf(o - m);
-        const float e64 = __expf(o64 - m);
-        float ssum = e;
+            for (int off = 32; off > 0; off >>= 1) o64 += __shfl_xor(o64, off);
+            if (lane == 0) s64[b] = o64 + hp[HL.plb + 64];
+        } else {
+            // value: 1x1 conv (C->1) + BN + ReLU
+            float v = hp[HL.vcb];
+            for (int c8 = 0; c8 < C / 8; ++c8) {
+                const u32x4_t q = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
+                const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) ssum += __shfl_xor(ssum, off);
-        ssum += e64;
-        const float inv = 1.0f / ssum;
-        policy[(size_t)gr * 65 + lane] = e * inv;
-        if (lane == 0) policy[(size_t)gr * 65 + 64] = e64 * inv;
-    } else {
-        // value head: 1x1 conv (C->1) + BN + ReLU, Linear(64->hidden), ReLU, Linear(hidden->1), tanh
-        float v = hp[HL.vcb];
-        for (int c8 = 0; c8 < C / 8; ++c8) {
-            const u32x4_t q = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
-            const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float x = from_act<DT>((w4[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
-                v += x * hp[HL.vcw + c8 * 8 + e];
+                for (int e = 0; e < 8; ++e) {
+                    const float x = from_act<DT>((w4[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
+                    v = __builtin_fmaf(x, cw[2 * C + c8 * 8 + e], v);
+                }
             }
+            sv[lane * B + b] = fmaxf(v, 0.0f);
         }
-        v = fmaxf(v, 0.0f);
-        const float* v1w = hp + HL.v1w;
-        float part = 0.0f;
-        for (int j0 = 0; j0 < N.hidden; j0 += 64) {
-            const bool ok = j0 + lane < N.hidden;
-            const int j = ok ? j0 + lane : N.hidden - 1;
-            float hj = hp[HL.v1b + j];
-            for (int s = 0; s < 64; ++s) {
-                const float xs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), s));
-                hj += v1w[s * N.hidden + j] * xs;
-            }
-            hj = fmaxf(hj, 0.0f);
-            part += ok ? hj * hp[HL.v2w + j] : 0.0f;
-        }
+    }
+    __syncthreads();
+    for (int task = wave; task < ntask; task += NW) {
+        float acc[B];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
-        if (lane == 0) value[gr] = tanhf(part + hp[HL.v2b]);
+        for (int b = 0; b < B; ++b) acc[b] = 0.0f;
+        if (task != wave) task_weights(task, wv);
+        if (task < 4) {  // policy Linear(128->64 of 65), inputs 32*task ..
+            const float* x = sp + task * 32 * B;
+#pragma unroll
+            for (int k = 0; k < 32; ++k)
+#pragma unroll
+                for (int b = 0; b < B; ++b) acc[b] = __builtin_fmaf(wv[k], x[k * B + b], acc[b]);
+#pragma unroll
+            for (int b = 0; b < B; ++b) pp[(task * B + b) * 64 + lane] = acc[b];
+        } else {  // value Linear(64->hidden), units 64*q + lane, inputs 32*c ..
+            const int t = task - 4, c = t & 1, q = t >> 1;
+            const int j = q * 64 + lane;
+            const float* x = sv + c * 32 * B;
+#pragma unroll
+            for (int k = 0; k < 32; ++k)
+#pragma unroll
+                for (int b = 0; b < B; ++b) acc[b] = __builtin_fmaf(wv[k], x[k * B + b], acc[b]);
+#pragma unroll
+            for (int b = 0; b < B; ++b) pv[(c * B + b) * nvs * 64 + j] = acc[b];
+        }
+    }
+    __syncthreads();
+    for (int job = wave; job < 2 * B; job += NW) {
+        const int b = job % B;
+        const int gr = row0 + b;
+        if (gr >= rows) continue;
+        if (job < B) {
+            const float o = hp[HL.plb + lane] + (((pp[(0 * B + b) * 64 + lane] + pp[(1 * B + b) * 64 + lane]) +
+                                                  pp[(2 * B + b) * 64 + lane]) +
+                                                 pp[(3 * B + b) * 64 + lane]);
+            const float o64 = s64[b];
+            float m = o;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+            m = fmaxf(m, o64);
+            const float e = __expf(o - m);
+            const float e64 = __expf(o64 - m);
+            float ssum = e;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) ssum += __shfl_xor(ssum, off);
+            ssum += e64;
+            const float inv = 1.0f / ssum;
+            policy[(size_t)gr * 65 + lane] = e * inv;
+            if (lane == 0) policy[(size_t)gr * 65 + 64] = e64 * inv;
+        } else {
+            // Linear(hidden->1) over ReLU(Linear(64->hidden)), tanh
+            float part = 0.0f;
+            for (int q = 0; q < nvs; ++q) {
+                const int j = q * 64 + lane;
+                if (j < hid) {
+                    const float h = hp[HL.v1b + j] + (pv[(0 * B + b) * nvs * 64 + j] + pv[(1 * B + b) * nvs * 64 + j]);
+                    part = __builtin_fmaf(fmaxf(h, 0.0f), hp[HL.v2w + j], part);
+                }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+            if (lane == 0) value[gr] = tanhf(part + hp[HL.v2b]);
+        }
     }
 }
 
@@ -496,7 +584,7 @@ __device__ __forceinline__ void load_bias(float4 (&bv)[G::NT], const NetView& N,
 // ABL != 0 only in diagnostic ablation builds (OAMD_RESNET_ABLATE, wrong results):
 // bit 0 = no in-loop barrier/DMA wait, 1 = no activation fragment reads,
 // 16 = no epilogue stores (accumulators keep running into the next layer),
-// 2 = no weight fragment reads, 3 = no in-loop weight DMA
+// 2 = no weight fragment reads, 3 = no in-loop weight DMA, 5 (32) = no heads
 template <class G, int DT, int IN, int ABL = 0>
 __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __restrict__ feat_in,
                                                     int fw, int H, int rows,
@@ -813,10 +901,9 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
         conv(std::integral_constant<int, 1>{}, 1 + 2 * blk);
         conv(std::integral_constant<int, 2>{}, 2 + 2 * blk);
     }
-    __syncthreads();
-    // (board, head) jobs: 2 per board, spread over the waves
-    for (int job = wave; job < 2 * G::BOARDS; job += G::WAVES)
-        heads<G, DT>(N, act, job, lane, row0, rows, policy, value);
+    __syncthreads();  // also drains this wave's trailing ring DMAs: the ring is free
+    if constexpr (ABL & 32) return;
+    heads<G, DT>(N, act, ring, wave, lane, row0, rows, policy, value);
 }
 
 template <class G, int DT, int IN, int ABL = 0>
@@ -867,6 +954,7 @@ static void dispatch(const NetView& N, const void* feat, int fw, int H, int rows
                 case 9: return launch_t<Geo<128>, OAMD_BF16, IN, 9>(N, feat, fw, H, rows, pol, val, s);
                 case 15: return launch_t<Geo<128>, OAMD_BF16, IN, 15>(N, feat, fw, H, rows, pol, val, s);
                 case 16: return launch_t<Geo<128>, OAMD_BF16, IN, 16>(N, feat, fw, H, rows, pol, val, s);
+                case 32: return launch_t<Geo<128>, OAMD_BF16, IN, 32>(N, feat, fw, H, rows, pol, val, s);
                 default: break;
             }
         }
