@@ -36,8 +36,14 @@ UNITS = {
     "capi.hip": EXACT,
     # accumulators and fragments in arch VGPRs: the default heuristic parks the
     # 128 accumulators of a 1-wave/SIMD tile in AGPRs and shuffles them per MFMA
-    "resnet.hip": os.environ.get("OAMD_RESNET_FLAGS", "-mllvm -amdgpu-mfma-vgpr-form=1").split(),
+    "resnet.hip": os.environ.get("OAMD_RESNET_FLAGS", "-mllvm -amdgpu-mfma-vgpr-form=1").split()
+    + ["-Rpass-analysis=kernel-resource-usage"],
 }
+
+
+# k_resnet_w8 (8 waves, 2 per SIMD) must allocate <= 208 VGPRs per wave so one
+# k_select wave (93 VGPRs) still fits beside it on each SIMD (resnet.hip)
+W8_VGPR_LIMIT = 208
 
 
 def run(cmd: list[str]) -> None:
@@ -45,8 +51,28 @@ def run(cmd: list[str]) -> None:
     if r.returncode != 0:
         sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
         raise SystemExit(f"build failed: {cmd[-1]}")
-    if r.stderr.strip():
+    if "kernel-resource-usage" in " ".join(cmd):
+        check_w8_vgprs(r.stderr)
+    elif r.stderr.strip():
         sys.stderr.write(r.stderr)
+
+
+def check_w8_vgprs(remarks: str) -> None:
+    """Parse -Rpass-analysis=kernel-resource-usage remarks; fail if a k_resnet_w8
+    instantiation's VGPR allocation (granule 8) exceeds W8_VGPR_LIMIT."""
+    name = None
+    seen = 0
+    for ln in remarks.splitlines():
+        if "Function Name:" in ln:
+            name = ln.split("Function Name:")[1].split()[0]
+        elif name and "k_resnet_w8" in name and " VGPRs:" in ln:
+            v = int(ln.split("VGPRs:")[1].split()[0])
+            seen += 1
+            if (v + 7) // 8 * 8 > W8_VGPR_LIMIT and os.environ.get("OAMD_W8_VGPR_CHECK", "1") != "0":
+                raise SystemExit(f"build failed: {name} uses {v} VGPRs (> {W8_VGPR_LIMIT}): "
+                                 "k_select could no longer co-reside with the ResNet kernel")
+    if not seen:  # A/B builds with other geometries (e.g. -DOAMD_WC=128) have no w8 kernel
+        sys.stderr.write("note: no k_resnet_w8 kernel in this build\n")
 
 
 def newer(out: Path, deps: list[Path]) -> bool:

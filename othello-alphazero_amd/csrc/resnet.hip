@@ -91,6 +91,9 @@ constexpr int kLdsBytes = 160 * 1024;
 #ifndef OAMD_ILV
 #define OAMD_ILV 1
 #endif
+#ifndef OAMD_VGPR_CAP
+#define OAMD_VGPR_CAP 208
+#endif
 // MFMAs of a step over which OAMD_ILV=1 spreads the step's fragment reads
 #ifndef OAMD_ILV_SPAN
 #define OAMD_ILV_SPAN 16
@@ -423,6 +426,20 @@ __host__ __device__ constexpr int head_scratch_floats(int hidden) {
     return 128 * B + 64 * B + 4 + 4 * B * 64 + 2 * B * ((hidden + 63) / 64) * 64 + 3 * 256 + 4;
 }
 
+// acc[b] += sum_k w[k] x[k][b], k in order; x in LDS ([k][B], broadcast reads),
+// in chunks of 8 inputs so the reads of one chunk are live at a time
+template <int B>
+__device__ __forceinline__ void dot32(float (&acc)[B], const float (&w)[32], const float* x) {
+#pragma unroll
+    for (int k0 = 0; k0 < 32; k0 += 8) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = k0; k < k0 + 8; ++k)
+#pragma unroll
+            for (int b = 0; b < B; ++b) acc[b] = __builtin_fmaf(w[k], x[k * B + b], acc[b]);
+    }
+}
+
 template <class G, int DT>
 __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act, unsigned char* scratch, int wave,
                                       int lane, int row0, int rows, float* __restrict__ policy,
@@ -431,6 +448,9 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
     constexpr int B = G::BOARDS;
     constexpr int NW = G::WAVES;
     static_assert(head_scratch_floats<B>(kMaxValueHidden) * 4 <= G::RING * G::STAGE, "head scratch");
+    // opaque to the optimiser: keeps the heads' lane-derived addresses from
+    // being hoisted to the kernel start and held live through the tower
+    asm volatile("" : "+v"(lane));
     const HeadLayout HL(C, N.hidden);
     const float* hp = N.head;
     const int hid = N.hidden;
@@ -474,6 +494,7 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
             // policy: 1x1 conv (C->2) + BN + ReLU; flatten c*64+s
             const float u0 = hp[HL.plw + lane * 65 + 64], u1 = hp[HL.plw + (64 + lane) * 65 + 64];
             float h0 = hp[HL.pcb + 0], h1 = hp[HL.pcb + 1];
+#pragma unroll 2
             for (int c8 = 0; c8 < C / 8; ++c8) {
                 const u32x4_t v = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
                 const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
@@ -495,6 +516,7 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
         } else {
             // value: 1x1 conv (C->1) + BN + ReLU
             float v = hp[HL.vcb];
+#pragma unroll 2
             for (int c8 = 0; c8 < C / 8; ++c8) {
                 const u32x4_t q = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
                 const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
@@ -515,20 +537,14 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
         if (task != wave) task_weights(task, wv);
         if (task < 4) {  // policy Linear(128->64 of 65), inputs 32*task ..
             const float* x = sp + task * 32 * B;
-#pragma unroll
-            for (int k = 0; k < 32; ++k)
-#pragma unroll
-                for (int b = 0; b < B; ++b) acc[b] = __builtin_fmaf(wv[k], x[k * B + b], acc[b]);
+            dot32<B>(acc, wv, x);
 #pragma unroll
             for (int b = 0; b < B; ++b) pp[(task * B + b) * 64 + lane] = acc[b];
         } else {  // value Linear(64->hidden), units 64*q + lane, inputs 32*c ..
             const int t = task - 4, c = t & 1, q = t >> 1;
             const int j = q * 64 + lane;
             const float* x = sv + c * 32 * B;
-#pragma unroll
-            for (int k = 0; k < 32; ++k)
-#pragma unroll
-                for (int b = 0; b < B; ++b) acc[b] = __builtin_fmaf(wv[k], x[k * B + b], acc[b]);
+            dot32<B>(acc, wv, x);
 #pragma unroll
             for (int b = 0; b < B; ++b) pv[(c * B + b) * nvs * 64 + j] = acc[b];
         }
@@ -586,10 +602,8 @@ __device__ __forceinline__ void load_bias(float4 (&bv)[G::NT], const NetView& N,
 // 16 = no epilogue stores (accumulators keep running into the next layer),
 // 2 = no weight fragment reads, 3 = no in-loop weight DMA, 5 (32) = no heads
 template <class G, int DT, int IN, int ABL = 0>
-__global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __restrict__ feat_in,
-                                                    int fw, int H, int rows,
-                                                    float* __restrict__ policy,
-                                                    float* __restrict__ value) {
+__device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ feat_in, int fw, int H, int rows,
+                                            float* __restrict__ policy, float* __restrict__ value) {
     constexpr int C = G::C;
     constexpr int kNT = G::NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -907,17 +921,35 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
 }
 
 template <class G, int DT, int IN, int ABL = 0>
+__global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __restrict__ feat_in, int fw, int H,
+                                                    int rows, float* __restrict__ policy, float* __restrict__ value) {
+    resnet_body<G, DT, IN, ABL>(N, feat_in, fw, H, rows, policy, value);
+}
+// The 8-wave (2 per SIMD) geometry capped at 208 VGPRs: that leaves 96 of a
+// SIMD's 512 for one k_select wave (93 VGPRs, no LDS), so the other pipeline
+// group's tree kernel co-resides with this kernel instead of waiting for a CU.
+template <class G, int DT, int IN, int ABL = 0>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_num_vgpr(OAMD_VGPR_CAP))) void k_resnet_w8(
+    NetView N, const void* __restrict__ feat_in, int fw, int H, int rows, float* __restrict__ policy,
+    float* __restrict__ value) {
+    resnet_body<G, DT, IN, ABL>(N, feat_in, fw, H, rows, policy, value);
+}
+
+template <class G, int DT, int IN, int ABL = 0>
 static void launch_t(const NetView& N, const void* feat, int fw, int H, int rows, float* pol,
                      float* val, hipStream_t s) {
     const unsigned grid = (unsigned)((rows + G::BOARDS - 1) / G::BOARDS);
+    constexpr auto kern = [] {
+        if constexpr (G::THREADS == 512) return &k_resnet_w8<G, DT, IN, ABL>;
+        else return &k_resnet<G, DT, IN, ABL>;
+    }();
     static bool configured = false;
     if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_resnet<G, DT, IN, ABL>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  G::LDS);
         configured = true;
     }
-    hipLaunchKernelGGL((k_resnet<G, DT, IN, ABL>), dim3(grid), dim3(G::THREADS), G::LDS, s, N, feat, fw, H,
-                       rows, pol, val);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(G::THREADS), G::LDS, s, N, feat, fw, H, rows, pol, val);
 }
 
 #ifdef OAMD_ABLATION
