@@ -138,8 +138,8 @@ def main() -> None:
     ap.add_argument("--hidden", type=int, default=128)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--eval-batch", type=int, default=0,
-                    help="NN rows per launch (games split into games*L/eval_batch pipeline groups; "
-                         "0 = the engine's default of 2 groups); configs[4] uses 2048")
+                    help="NN rows per ResNet launch (0 = a whole pipeline group, games*L/2 rows); "
+                         "configs[4] uses 2048")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
@@ -169,11 +169,8 @@ def main() -> None:
                        num_threads=args.threads, batch_size=args.batch, seed=engine_seed)
     b.random_openings(8, seed=opening_seed)
     L = args.threads * args.batch
-    if args.eval_batch:
-        groups, rem = divmod(args.games * L, args.eval_batch)
-        if rem or not 1 <= groups <= 8:
-            raise SystemExit(f"--eval-batch must divide games*L = {args.games * L} into 1..8 groups")
-        b.engine.set_pipeline(groups)
+    if args.eval_batch:  # rows per ResNet launch; the 2 pipeline groups stay
+        b.engine.set_nn_batch(args.eval_batch)
     sims_per_search = L * ((args.sims + L - 1) // L)
 
     def step():

@@ -158,6 +158,11 @@ int oamd_engine_search(oamd_engine *e, oamd_net *net, int64_t *simulations, int6
  * kernels of one group overlap the NN launch of another (0 = auto: 2 groups
  * from 64 games, else 1; at most 8). Results do not depend on it. */
 int oamd_engine_set_pipeline(oamd_engine *e, int32_t groups);
+/* Rows per ResNet launch in oamd_engine_search (0 = a whole pipeline group per
+ * launch): a group's rows are evaluated by consecutive launches of at most
+ * `rows` rows on its stream (the NN evaluation batch; configs[4] uses 2048).
+ * Results do not depend on it. */
+int oamd_engine_set_nn_batch(oamd_engine *e, int32_t rows);
 
 /* Step-wise search for an external evaluator (the Python NeuralNet callback
  * path, othello_mcts.cpp:36-45). Rows: row = game * L + leaf, L =

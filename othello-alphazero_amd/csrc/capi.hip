@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -12,6 +13,7 @@
 
 #include "../../include/othello_mcts_amd.h"
 #include "bitboard.h"
+
 #include "engine.h"
 #include "kernels.h"
 
@@ -154,6 +156,9 @@ struct oamd_engine {
     int step_phase = 0;  // 0 = expect select, 1 = expect backup
     // pipeline groups (0 = auto) and their streams / fork-join events
     int pipeline = 0;
+    // rows per k_resnet launch (0 = one launch per group and step); a group's
+    // rows are evaluated by consecutive launches on its stream
+    int nn_batch = 0;
     int n_pipe_streams = 0;
     hipStream_t pipe_stream[kMaxPipeline] = {};
     hipEvent_t fork_ev = nullptr;
@@ -168,6 +173,7 @@ struct oamd_engine {
     bool timing = false;
     std::vector<hipEvent_t> ev[2];
     int ev_blocks[2] = {0, 0};  // pending (step, group) blocks per pool
+    int64_t ev_launches[2] = {0, 0};  // k_resnet launches inside those blocks
     int64_t ev_rows[2] = {0, 0};
     int ev_cur = 0;
     float nn_ms = 0.0f;
@@ -190,7 +196,7 @@ struct oamd_engine {
             HIPCHK(hipEventElapsedTime(&ms, b[4], b[5]));
             backup_ms += ms;
         }
-        nn_launches += n;
+        nn_launches += ev_launches[p];
         nn_rows += ev_rows[p];
         ev_blocks[p] = 0;
         return OAMD_OK;
@@ -840,8 +846,11 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
                 HIPCHK(hipStreamWaitEvent(st[k], e->nn_token, 0));
             }
             if (ev) HIPCHK(hipEventRecord(ev[2], ns));
-            launch_resnet_packed(N, E.feat + r0 * E.FW, E.FW, E.H, ng[k] * L, E.policy + r0 * 65, E.value + r0,
-                                 ns);
+            const int grows = ng[k] * L;
+            const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
+            for (int r = 0; r < grows; r += cb)
+                launch_resnet_packed(N, E.feat + (r0 + r) * E.FW, E.FW, E.H, std::min(cb, grows - r),
+                                     E.policy + (r0 + r) * 65, E.value + r0 + r, ns);
             if (ev) HIPCHK(hipEventRecord(ev[3], ns));
             if (K > 1 && OAMD_NN_ORDER == 2) {
                 HIPCHK(hipEventRecord(e->nn_ev[k], ns));
@@ -863,6 +872,12 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     }
     if (e->timing) {
         e->ev_blocks[pool] = steps * K;
+        int64_t nl = 0;
+        for (int k = 0; k < K; ++k) {
+            const int grows = ng[k] * L, cb = e->nn_batch > 0 ? e->nn_batch : grows;
+            nl += (grows + cb - 1) / cb;
+        }
+        e->ev_launches[pool] = (int64_t)steps * nl;
         e->ev_rows[pool] = (int64_t)steps * e->G * L;
         e->ev_cur ^= 1;
     }
@@ -883,6 +898,12 @@ int oamd_engine_set_pipeline(oamd_engine* e, int32_t groups) {
     if (groups < 0 || groups > kMaxPipeline)
         return fail(OAMD_INVALID_ARGUMENT, "pipeline groups must be in [0, " + std::to_string(kMaxPipeline) + "]");
     e->pipeline = groups;
+    return OAMD_OK;
+}
+
+int oamd_engine_set_nn_batch(oamd_engine* e, int32_t rows) {
+    if (rows < 0) return fail(OAMD_INVALID_ARGUMENT, "nn batch rows must be >= 0");
+    e->nn_batch = rows;
     return OAMD_OK;
 }
 

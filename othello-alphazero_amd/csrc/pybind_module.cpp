@@ -619,6 +619,7 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
              })
         .def("enable_timing", [](Engine& e, bool on) { check(oamd_engine_enable_timing(e.h, on ? 1 : 0)); })
         .def("set_pipeline", [](Engine& e, int groups) { check(oamd_engine_set_pipeline(e.h, groups)); })
+        .def("set_nn_batch", [](Engine& e, int rows) { check(oamd_engine_set_nn_batch(e.h, rows)); })
         .def("nn_timing", [](Engine& e) {
             float ms;
             int64_t launches, rows;

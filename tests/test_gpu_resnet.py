@@ -167,6 +167,27 @@ def test_pipeline_groups_do_not_change_results(om):
     assert runs[0] == runs[1] == runs[2] == runs[3]
 
 
+def test_nn_batch_does_not_change_results(om):
+    """Evaluating a group's rows in several ResNet launches (oamd_engine_set_nn_batch,
+    configs[4]'s eval batch) changes no game's statistics."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(17, 9, 128, 2, 32), device=0)
+    kw = dict(history_size=4, num_simulations=96, num_threads=2, batch_size=8, seed=9,
+              node_capacity=1 << 15)
+    runs = []
+    for rows in (0, 64, 100):
+        b = om.BatchedMCTS(12, **kw)
+        b.engine.set_nn_batch(rows)
+        b.random_openings(5, seed=3)
+        for _ in range(2):
+            b.search(net)
+            b.selfplay_move(temperature_moves=12, opening_moves=2)
+        b.search(net)
+        runs.append([(b.visit_counts(g), b.mean_action_values(g)) for g in range(12)])
+    assert runs[0] == runs[1] == runs[2]
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("C,R", [(128, 9), (256, 3)])
 def test_small_batch_geometry_is_bit_identical(om, dtype, C, R):
