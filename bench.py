@@ -264,7 +264,7 @@ def main() -> None:
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "k_resnet (fused 19-conv tower + heads)",
+            "kernel": "k_resnet_w8 (fused 19-conv tower + heads, 8-wave geometry)",
             "achieved": round(achieved, 2),
             "peak": peak,
             "unit": "TFLOP/s",

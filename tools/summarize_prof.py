@@ -38,7 +38,7 @@ def main(tag: str) -> None:
         k = kern.setdefault(name, {})
         for c, v in cs.items():
             k[c + "_per_launch"] = sum(v) / len(v)
-    res = kern.get("k_resnet", {})
+    res = next((v for k, v in kern.items() if k.startswith("k_resnet")), {})
     # the bench line of the traced run names the workload the counters belong to
     bench_line = None
     log = PROF / "trace.log"
