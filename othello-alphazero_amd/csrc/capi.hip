@@ -901,6 +901,13 @@ int oamd_engine_set_pipeline(oamd_engine* e, int32_t groups) {
     return OAMD_OK;
 }
 
+int oamd_debug_read_stamps(uint64_t* out, int64_t n) {
+    if (!out || n < 0) return fail(OAMD_INVALID_ARGUMENT, "stamps: bad buffer");
+    const int rc = resnet_read_stamps(reinterpret_cast<unsigned long long*>(out), (long long)n);
+    if (rc == -2) return fail(OAMD_INVALID_ARGUMENT, "built without OAMD_STAMPS");
+    return rc ? fail(OAMD_RUNTIME, "stamp copy failed") : OAMD_OK;
+}
+
 int oamd_engine_set_nn_batch(oamd_engine* e, int32_t rows) {
     if (rows < 0) return fail(OAMD_INVALID_ARGUMENT, "nn batch rows must be >= 0");
     e->nn_batch = rows;

@@ -60,6 +60,8 @@ void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* pol
                        hipStream_t s);
 size_t resnet_packed_weight_elems(int C, int R);
 size_t resnet_head_floats(int C, int hidden);
+// diagnostic stamp buffer (OAMD_STAMPS builds; -2 otherwise), see resnet.hip
+int resnet_read_stamps(unsigned long long* out, long long n);
 // Weight K-step schedule shared by the kernel and the host packer: a K-step is
 // one 3x3 tap x 32 input channels. K-steps per conv (first conv: input zero-
 // padded to 32 channels, 9 K-steps rounded up to whole weight stages with

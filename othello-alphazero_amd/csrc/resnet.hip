@@ -61,6 +61,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 #define OAMD_WC256 128
 #endif
 constexpr int kLdsBytes = 160 * 1024;
+constexpr int kMaxStampWgs = 1 << 16;
 // Weight stage = 16 KiB (2 K-steps at C=128, 1 at C=256) in a 3-slot ring.
 // Compile-time schedule knobs, A/B-measured on MI355X with tools/ab.sh (same box,
 // k_resnet 8192 rows, C=128): 16 KiB stages beat 8 KiB stages in a 6-slot ring
@@ -601,6 +602,32 @@ __device__ __forceinline__ void load_bias(float4 (&bv)[G::NT], const NetView& N,
 // bit 0 = no in-loop barrier/DMA wait, 1 = no activation fragment reads,
 // 16 = no epilogue stores (accumulators keep running into the next layer),
 // 2 = no weight fragment reads, 3 = no in-loop weight DMA, 5 (32) = no heads
+#ifdef OAMD_STAMPS
+// Diagnostic build only (tools/nn_stamps.py): per workgroup, wave 0 lane 0
+// records s_memrealtime (100 MHz) at kernel entry, after the prologue barrier,
+// after the tower, and at exit, plus s_memtime cycles across the tower and the
+// hardware id of its CU. Nothing else reads this buffer.
+__device__ unsigned long long g_oamd_stamps[kMaxStampWgs * 8];
+__device__ __forceinline__ void stamp(int slot, int wave, int lane) {
+    if (wave == 0 && lane == 0 && blockIdx.x < kMaxStampWgs) {
+        __builtin_amdgcn_sched_barrier(0);
+        g_oamd_stamps[blockIdx.x * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+        if (slot == 1 || slot == 2) g_oamd_stamps[blockIdx.x * 8 + 4 + slot] = __builtin_amdgcn_s_memtime();
+        if (slot == 0) {
+            unsigned id;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            g_oamd_stamps[blockIdx.x * 8 + 4] = ((unsigned long long)xcc << 32) | id;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+#define OAMD_STAMP(slot) stamp(slot, wave, lane)
+#else
+#define OAMD_STAMP(slot) ((void)0)
+#endif
+
 template <class G, int DT, int IN, int ABL = 0>
 __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ feat_in, int fw, int H, int rows,
                                             float* __restrict__ policy, float* __restrict__ value) {
@@ -617,6 +644,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     const int wn = wave % G::WN;  // OAMD_WC-channel block of this wave
     const int kg = lane >> 4;
     const int row0 = blockIdx.x * G::BOARDS;
+    OAMD_STAMP(0);
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
     const int total = (ksteps_first(C) + 2 * N.R * ksteps_tower(C)) / G::KS;
 
@@ -659,18 +687,27 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         const int gr = row0 + b;
         const uint32_t one = to_act<DT>(1.0f);
         uint32_t words[16];  // 32 channels as 16-bit pairs
+        // one global round trip per board: the wave of board b (lane = square)
+        // issues all its input loads before using any of them
         if constexpr (IN == kPacked) {
             uint32_t mask = 0;  // bit c = channel c is 1 (c < 31)
-            if (gr < rows) {
+            if (gr < rows) {    // wave-uniform
+                // lane j holds word j of the row (fw = 2 + 2H <= 32 words)
                 const uint64_t* fr = reinterpret_cast<const uint64_t*>(feat_in) + (size_t)gr * fw;
-                const uint64_t meta = fr[0];
+                const uint64_t wj = fr[p < fw ? p : fw - 1];
+                const uint32_t lo = (uint32_t)wj, hi = (uint32_t)(wj >> 32);
+                auto word = [&](int j) {
+                    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, j) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)lo, j);
+                };
+                const uint64_t meta = word(0);
                 if ((meta >> 16) & 1ULL) {
                     const int t = (int)((meta >> 8) & 7ULL);
                     const int src = inverse_transform(p, t);
                     mask = (uint32_t)(meta & 1ULL);
                     for (int h = 0; h < H; ++h) {
-                        mask |= (uint32_t)((fr[2 + 2 * h] >> (63 - src)) & 1ULL) << (1 + 2 * h);
-                        mask |= (uint32_t)((fr[3 + 2 * h] >> (63 - src)) & 1ULL) << (2 + 2 * h);
+                        mask |= (uint32_t)((word(2 + 2 * h) >> (63 - src)) & 1ULL) << (1 + 2 * h);
+                        mask |= (uint32_t)((word(3 + 2 * h) >> (63 - src)) & 1ULL) << (2 + 2 * h);
                     }
                 }
             }
@@ -681,13 +718,19 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 words[w] = lo | (hi << 16);
             }
         } else {
-            const float* fr = reinterpret_cast<const float*>(feat_in) + (size_t)gr * N.cin * 64;
-            const bool ok = gr < rows;
+            float v[32];
+#pragma unroll
+            for (int c = 0; c < 32; ++c) v[c] = 0.0f;
+            if (gr < rows) {  // wave-uniform; channel index clamped so all 32 loads issue at once
+                const float* fr = reinterpret_cast<const float*>(feat_in) + (size_t)gr * N.cin * 64;
+#pragma unroll
+                for (int c = 0; c < 32; ++c) v[c] = fr[(c < N.cin ? c : N.cin - 1) * 64 + p];
+            }
 #pragma unroll
             for (int w = 0; w < 16; ++w) {
                 const int c0 = 2 * w, c1 = 2 * w + 1;
-                const uint32_t lo = (ok && c0 < N.cin) ? to_act<DT>(fr[c0 * 64 + p]) : 0u;
-                const uint32_t hi = (ok && c1 < N.cin) ? to_act<DT>(fr[c1 * 64 + p]) : 0u;
+                const uint32_t lo = c0 < N.cin ? to_act<DT>(v[c0]) : 0u;
+                const uint32_t hi = c1 < N.cin ? to_act<DT>(v[c1]) : 0u;
                 words[w] = lo | (hi << 16);
             }
         }
@@ -705,10 +748,12 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     int g = 0;     // stage holding the current K-step
     int slot = 0;  // g % RING
 
+    OAMD_STAMP(7);
     // stage 0 and the input planes must be visible (bias loads are older than the DMAs)
     if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();
     lds_barrier();
     load_frags(fa, act, ring, kstep_offset<C>(0, true), rd, wl);
+    OAMD_STAMP(1);
 
     const int nlayers = 1 + 2 * N.R;
     // one conv layer: KIND 0 = first conv, 1 = a block's first conv (saves the
@@ -916,8 +961,10 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         conv(std::integral_constant<int, 2>{}, 2 + 2 * blk);
     }
     __syncthreads();  // also drains this wave's trailing ring DMAs: the ring is free
+    OAMD_STAMP(2);
     if constexpr (ABL & 32) return;
     heads<G, DT>(N, act, ring, wave, lane, row0, rows, policy, value);
+    OAMD_STAMP(3);
 }
 
 template <class G, int DT, int IN, int ABL = 0>
@@ -1029,6 +1076,19 @@ void launch_resnet_packed(const NetView& N, const uint64_t* feat, int fw, int H,
 void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* policy, float* value,
                        hipStream_t s) {
     dispatch<kF32>(N, feat, 0, 0, rows, policy, value, s);
+}
+
+int resnet_read_stamps(unsigned long long* out, long long n) {
+#ifdef OAMD_STAMPS
+    if (n > (long long)kMaxStampWgs * 8) n = (long long)kMaxStampWgs * 8;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oamd_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? 0
+               : -1;
+#else
+    (void)out;
+    (void)n;
+    return -2;
+#endif
 }
 
 }  // namespace oamd
