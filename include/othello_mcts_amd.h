@@ -164,8 +164,7 @@ int oamd_engine_set_pipeline(oamd_engine *e, int32_t groups);
  * Results do not depend on it. */
 int oamd_engine_set_nn_batch(oamd_engine *e, int32_t rows);
 /* Diagnostics: copy the ResNet kernel's per-workgroup time stamps (8 u64 per
- * workgroup: realtime at entry / after prologue / after tower / exit, hardware
- * id, cycles after prologue / after tower) of the last launch. Only in builds
+ * workgroup, 16 u64 per workgroup: see tools/nn_stamps.py) of the last launch. Only in builds
  * with OAMD_EXTRA_FLAGS=-DOAMD_STAMPS; otherwise OAMD_INVALID_ARGUMENT. */
 int oamd_debug_read_stamps(uint64_t *out, int64_t n);
 

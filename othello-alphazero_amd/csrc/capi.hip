@@ -329,6 +329,7 @@ struct oamd_net {
     uint16_t* w = nullptr;
     float* bias = nullptr;
     float* head = nullptr;
+    uint16_t* hconv = nullptr;
     bool loaded = false;
     std::vector<std::string> keys;
     std::vector<int64_t> numel;
@@ -343,6 +344,7 @@ struct oamd_net {
         N.w = w;
         N.bias = bias;
         N.head = head;
+        N.hconv = hconv;
         return N;
     }
     ~oamd_net() {
@@ -350,6 +352,7 @@ struct oamd_net {
         dfree(w);
         dfree(bias);
         dfree(head);
+        dfree(hconv);
     }
 };
 
@@ -434,7 +437,8 @@ int oamd_net_create(int32_t device, const oamd_net_desc* d, oamd_net** out) {
     int rc;
     if ((rc = dalloc(&net->w, resnet_packed_weight_elems(C, R))) ||
         (rc = dalloc(&net->bias, (size_t)(1 + 2 * R) * C)) ||
-        (rc = dalloc(&net->head, resnet_head_floats(C, hid)))) {
+        (rc = dalloc(&net->head, resnet_head_floats(C, hid))) ||
+        (rc = dalloc(&net->hconv, resnet_hconv_elems(C)))) {
         delete net;
         return rc;
     }
@@ -604,7 +608,19 @@ int oamd_net_load_state(oamd_net* net, const float* const* t, int32_t n_tensors)
         for (int j = 0; j < hid; ++j) head[HL_v2w + j] = W2[j];
         head[HL_v2b] = B2[0];
     }
+    // 1x1 head convs (folded) in MFMA A-fragment order: lane holds row lane&15
+    // (0, 1 = policy channels, 2 = value, else 0) and input channels
+    // cb*32 + 8*chunk(lane>>4) + j, matching the tower's B fragments
+    std::vector<uint16_t> hconv(resnet_hconv_elems(C));
+    for (int cb = 0; cb < C / 32; ++cb)
+        for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; ++j) {
+                const int r = lane & 15, ci = cb * 32 + 8 * resnet_kgroup_chunk(lane >> 4) + j;
+                const float v = r < 2 ? head[HL_pcw + r * C + ci] : (r == 2 ? head[HL_vcw + ci] : 0.0f);
+                hconv[((size_t)cb * 64 + lane) * 8 + j] = d.dtype == OAMD_BF16 ? f32_to_bf16_rne(v) : f32_to_f16(v);
+            }
     DeviceGuard dg(net->device);
+    HIPCHK(hipMemcpy(net->hconv, hconv.data(), hconv.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(net->w, packed.data(), packed.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(net->bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(net->head, head.data(), head.size() * 4, hipMemcpyHostToDevice));

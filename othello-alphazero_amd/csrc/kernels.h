@@ -51,6 +51,7 @@ struct NetView {
     const uint16_t* w;   // packed conv weights, all layers, fragment order
     const float* bias;   // folded conv bias, (1 + 2R) * C
     const float* head;   // head parameters, see resnet.hip
+    const uint16_t* hconv;  // 1x1 head convs (BN folded), MFMA A fragments: [C/32][lane][8]
 };
 
 // features: packed engine rows (fw words per row, history H) or fp32 planes
@@ -60,6 +61,8 @@ void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* pol
                        hipStream_t s);
 size_t resnet_packed_weight_elems(int C, int R);
 size_t resnet_head_floats(int C, int hidden);
+// elements of the packed 1x1 head-conv fragments (NetView::hconv)
+inline size_t resnet_hconv_elems(int C) { return (size_t)(C / 32) * 64 * 8; }
 // diagnostic stamp buffer (OAMD_STAMPS builds; -2 otherwise), see resnet.hip
 int resnet_read_stamps(unsigned long long* out, long long n);
 // Weight K-step schedule shared by the kernel and the host packer: a K-step is

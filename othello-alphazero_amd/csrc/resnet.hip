@@ -93,7 +93,7 @@ constexpr int kMaxStampWgs = 1 << 16;
 #define OAMD_ILV 1
 #endif
 #ifndef OAMD_VGPR_CAP
-#define OAMD_VGPR_CAP 208
+#define OAMD_VGPR_CAP 104  // gfx950 counts the unified VGPR+AGPR file: 2 x 104 = 208
 #endif
 // MFMAs of a step over which OAMD_ILV=1 spreads the step's fragment reads
 #ifndef OAMD_ILV_SPAN
@@ -412,20 +412,46 @@ __device__ __forceinline__ void lds_barrier() {
 // Policy and value heads, all waves of the workgroup together (called by every
 // thread; barriers inside). The Linear layers run k-split with every board on
 // every lane, so a workgroup reads each head weight once (not once per board):
-//   phase 1  1x1 convs + BN + ReLU, one wave per (board, head), lane = square;
-//            results (and policy logit 64, a reduction over squares) go to
-//            `scratch`, the drained weight ring;
+//   phase 1  both 1x1 convs + BN + ReLU of a board as one MFMA GEMM
+//            (16 rows: 2 policy, 1 value, 13 zero) on one wave per board;
+//            results go to `scratch`, the drained weight ring;
 //   phase 2  partial dot products over 32-input chunks, lane = output unit,
 //            one task per (chunk, 64-unit slice);
-//   phase 3  per board: chunks summed in a fixed order, softmax(65) / ReLU,
-//            Linear(hidden->1), tanh.
+//   phase 3  per board: chunks summed in a fixed order, policy logit 64 (a
+//            reduction over squares), softmax(65) / ReLU, Linear(hidden->1), tanh.
 // Every output's arithmetic order is independent of BOARDS / WAVES, so all
 // geometries produce identical bits.
 constexpr int kMaxValueHidden = 1024;  // scratch budget (capi.hip validates)
 template <int B>
 __host__ __device__ constexpr int head_scratch_floats(int hidden) {
-    return 128 * B + 64 * B + 4 + 4 * B * 64 + 2 * B * ((hidden + 63) / 64) * 64 + 3 * 256 + 4;
+    return 128 * B + 64 * B + 4 * B * 64 + 2 * B * ((hidden + 63) / 64) * 64;
 }
+
+#ifdef OAMD_STAMPS
+// Diagnostic build only (tools/nn_stamps.py): per workgroup, wave 0 lane 0
+// records s_memrealtime (100 MHz) at kernel entry, after the prologue barrier,
+// after the tower, and at exit, plus s_memtime cycles across the tower and the
+// hardware id of its CU. Nothing else reads this buffer.
+__device__ unsigned long long g_oamd_stamps[kMaxStampWgs * 16];
+__device__ __forceinline__ void stamp(int slot, int wave, int lane) {
+    if (wave == 0 && lane == 0 && blockIdx.x < kMaxStampWgs) {
+        __builtin_amdgcn_sched_barrier(0);
+        g_oamd_stamps[blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+        if (slot == 1 || slot == 2) g_oamd_stamps[blockIdx.x * 16 + 4 + slot] = __builtin_amdgcn_s_memtime();
+        if (slot == 0) {
+            unsigned id;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            g_oamd_stamps[blockIdx.x * 16 + 4] = ((unsigned long long)xcc << 32) | id;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+#define OAMD_STAMP(slot) stamp(slot, wave, lane)
+#else
+#define OAMD_STAMP(slot) ((void)0)
+#endif
 
 // acc[b] += sum_k w[k] x[k][b], k in order; x in LDS ([k][B], broadcast reads),
 // in chunks of 8 inputs so the reads of one chunk are live at a time
@@ -458,10 +484,8 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
     const int nvs = (hid + 63) / 64;  // 64-unit slices of the value hidden layer
     float* sp = reinterpret_cast<float*>(scratch);  // [128][B] policy conv outputs (k = c*64 + square)
     float* sv = sp + 128 * B;                       // [64][B]  value conv outputs
-    float* s64 = sv + 64 * B;                       // [B]      policy logit 64 (with bias)
-    float* pp = s64 + 4;                            // [4][B][64] policy partials
+    float* pp = sv + 64 * B;                        // [4][B][64] policy partials
     float* pv = pp + 4 * B * 64;                    // [2][B][nvs*64] value partials
-    float* cw = pv + 2 * B * nvs * 64;              // 1x1 conv weights: pcw [2][C], vcw [C]
 
     // Linear weights of this wave's phase-2 task (one column of 32 inputs per
     // lane): task t < 4 covers policy inputs 32t.., task 4 + 2q + c value
@@ -483,59 +507,49 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
     };
     const int ntask = 4 + 2 * nvs;
     float wv[32];
-    if (wave < ntask) task_weights(wave, wv);
-    // the 1x1 conv weights go to LDS (one global round trip for the
-    // workgroup), so the conv loops below read them as LDS broadcasts
-    for (int i = wave * 64 + lane; i < 3 * C; i += NW * 64) cw[i] = hp[i < 2 * C ? HL.pcw + i : HL.vcw + i - 2 * C];
-    __syncthreads();
-    for (int job = wave; job < 2 * B; job += NW) {
-        const int b = job % B;
-        const unsigned char* arow = act + (b * G::BROWS + pad_row(lane)) * G::RP;
-        if (job < B) {
-            // policy: 1x1 conv (C->2) + BN + ReLU; flatten c*64+s
-            const float u0 = hp[HL.plw + lane * 65 + 64], u1 = hp[HL.plw + (64 + lane) * 65 + 64];
-            float h0 = hp[HL.pcb + 0], h1 = hp[HL.pcb + 1];
-#pragma unroll 2
-            for (int c8 = 0; c8 < C / 8; ++c8) {
-                const u32x4_t v = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
-                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    // waves without phase-1 work issue their first task's weights now
+    if (wave % G::WN != 0 && wave < ntask) task_weights(wave, wv);
+    OAMD_STAMP(8);
+    // phase 1: both 1x1 convs of a board as one small MFMA GEMM on the wave
+    // that owns the board's first channel block: A = folded head conv weights
+    // (rows 0, 1 = policy channels, row 2 = value, rows 3-15 zero; packed in
+    // fragment order on the host), B = the tower output at the centre tap.
+    if (wave % G::WN == 0) {
+        const int b = wave / G::WN;
+        u32x4_t hw[C / 32];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float x = from_act<DT>((w4[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
-                    h0 = __builtin_fmaf(x, cw[c8 * 8 + e], h0);
-                    h1 = __builtin_fmaf(x, cw[C + c8 * 8 + e], h1);
-                }
+        for (int cb = 0; cb < C / 32; ++cb)
+            hw[cb] = *reinterpret_cast<const u32x4_t*>(N.hconv + ((size_t)cb * 64 + lane) * 8);
+        int rd[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            rd[m] = (b * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) * G::RP + kgroup_chunk(lane >> 4) * 16;
+        f32x4_t d[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) d[m] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int cb = 0; cb < C / 32; ++cb)
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                d[m] = mfma<DT>(hw[cb], *reinterpret_cast<const u32x4_t*>(act + rd[m] + cb * 64), d[m]);
+        if (lane < 16) {  // rows 0-3 of output column `lane` of each position tile
+            const float pb0 = hp[HL.pcb + 0], pb1 = hp[HL.pcb + 1], vb = hp[HL.vcb];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int pos = kTilePos.p[16 * m + lane];
+                sp[pos * B + b] = fmaxf(d[m][0] + pb0, 0.0f);
+                sp[(64 + pos) * B + b] = fmaxf(d[m][1] + pb1, 0.0f);
+                sv[pos * B + b] = fmaxf(d[m][2] + vb, 0.0f);
             }
-            h0 = fmaxf(h0, 0.0f);
-            h1 = fmaxf(h1, 0.0f);
-            sp[lane * B + b] = h0;
-            sp[(64 + lane) * B + b] = h1;
-            float o64 = __builtin_fmaf(u1, h1, u0 * h0);
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) o64 += __shfl_xor(o64, off);
-            if (lane == 0) s64[b] = o64 + hp[HL.plb + 64];
-        } else {
-            // value: 1x1 conv (C->1) + BN + ReLU
-            float v = hp[HL.vcb];
-#pragma unroll 2
-            for (int c8 = 0; c8 < C / 8; ++c8) {
-                const u32x4_t q = *reinterpret_cast<const u32x4_t*>(arow + c8 * 16);
-                const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float x = from_act<DT>((w4[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
-                    v = __builtin_fmaf(x, cw[2 * C + c8 * 8 + e], v);
-                }
-            }
-            sv[lane * B + b] = fmaxf(v, 0.0f);
         }
     }
     __syncthreads();
+    OAMD_STAMP(9);
     for (int task = wave; task < ntask; task += NW) {
         float acc[B];
 #pragma unroll
         for (int b = 0; b < B; ++b) acc[b] = 0.0f;
-        if (task != wave) task_weights(task, wv);
+        if (task != wave || wave % G::WN == 0) task_weights(task, wv);
         if (task < 4) {  // policy Linear(128->64 of 65), inputs 32*task ..
             const float* x = sp + task * 32 * B;
             dot32<B>(acc, wv, x);
@@ -551,6 +565,7 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
         }
     }
     __syncthreads();
+    OAMD_STAMP(10);
     for (int job = wave; job < 2 * B; job += NW) {
         const int b = job % B;
         const int gr = row0 + b;
@@ -559,7 +574,12 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
             const float o = hp[HL.plb + lane] + (((pp[(0 * B + b) * 64 + lane] + pp[(1 * B + b) * 64 + lane]) +
                                                   pp[(2 * B + b) * 64 + lane]) +
                                                  pp[(3 * B + b) * 64 + lane]);
-            const float o64 = s64[b];
+            // policy logit 64: a reduction over squares (lane = square)
+            const float u0 = hp[HL.plw + lane * 65 + 64], u1 = hp[HL.plw + (64 + lane) * 65 + 64];
+            float o64 = __builtin_fmaf(u1, sp[(64 + lane) * B + b], u0 * sp[lane * B + b]);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) o64 += __shfl_xor(o64, off);
+            o64 += hp[HL.plb + 64];
             float m = o;
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
@@ -602,31 +622,6 @@ __device__ __forceinline__ void load_bias(float4 (&bv)[G::NT], const NetView& N,
 // bit 0 = no in-loop barrier/DMA wait, 1 = no activation fragment reads,
 // 16 = no epilogue stores (accumulators keep running into the next layer),
 // 2 = no weight fragment reads, 3 = no in-loop weight DMA, 5 (32) = no heads
-#ifdef OAMD_STAMPS
-// Diagnostic build only (tools/nn_stamps.py): per workgroup, wave 0 lane 0
-// records s_memrealtime (100 MHz) at kernel entry, after the prologue barrier,
-// after the tower, and at exit, plus s_memtime cycles across the tower and the
-// hardware id of its CU. Nothing else reads this buffer.
-__device__ unsigned long long g_oamd_stamps[kMaxStampWgs * 8];
-__device__ __forceinline__ void stamp(int slot, int wave, int lane) {
-    if (wave == 0 && lane == 0 && blockIdx.x < kMaxStampWgs) {
-        __builtin_amdgcn_sched_barrier(0);
-        g_oamd_stamps[blockIdx.x * 8 + slot] = __builtin_amdgcn_s_memrealtime();
-        if (slot == 1 || slot == 2) g_oamd_stamps[blockIdx.x * 8 + 4 + slot] = __builtin_amdgcn_s_memtime();
-        if (slot == 0) {
-            unsigned id;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
-            unsigned xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            g_oamd_stamps[blockIdx.x * 8 + 4] = ((unsigned long long)xcc << 32) | id;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-#define OAMD_STAMP(slot) stamp(slot, wave, lane)
-#else
-#define OAMD_STAMP(slot) ((void)0)
-#endif
 
 template <class G, int DT, int IN, int ABL = 0>
 __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ feat_in, int fw, int H, int rows,
@@ -975,6 +970,9 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
 // The 8-wave (2 per SIMD) geometry capped at 208 VGPRs: that leaves 96 of a
 // SIMD's 512 for one k_select wave (93 VGPRs, no LDS), so the other pipeline
 // group's tree kernel co-resides with this kernel instead of waiting for a CU.
+// amdgpu_num_vgpr counts in units of the unified VGPR+AGPR file on gfx950
+// (the backend doubles it), hence OAMD_VGPR_CAP = 104; build.py checks the
+// resulting allocation.
 template <class G, int DT, int IN, int ABL = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_num_vgpr(OAMD_VGPR_CAP))) void k_resnet_w8(
     NetView N, const void* __restrict__ feat_in, int fw, int H, int rows, float* __restrict__ policy,
@@ -1080,7 +1078,7 @@ void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* pol
 
 int resnet_read_stamps(unsigned long long* out, long long n) {
 #ifdef OAMD_STAMPS
-    if (n > (long long)kMaxStampWgs * 8) n = (long long)kMaxStampWgs * 8;
+    if (n > (long long)kMaxStampWgs * 16) n = (long long)kMaxStampWgs * 16;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oamd_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
                ? 0
                : -1;

@@ -27,10 +27,10 @@ for _ in range(20):
 torch.cuda.synchronize()
 lib = ctypes.CDLL(str(ROOT / "othello-alphazero_amd" / "othello_mcts" / "liboamd.so"))
 wgs = rows // 4
-buf = (ctypes.c_uint64 * (wgs * 8))()
-assert lib.oamd_debug_read_stamps(buf, ctypes.c_int64(wgs * 8)) == 0, "build with -DOAMD_STAMPS"
-s = np.frombuffer(buf, dtype=np.uint64).reshape(wgs, 8).astype(np.int64)
-t0, t1, t2, t3, hw, c1, c2, t7 = (s[:, i] for i in range(8))
+buf = (ctypes.c_uint64 * (wgs * 16))()
+assert lib.oamd_debug_read_stamps(buf, ctypes.c_int64(wgs * 16)) == 0, "build with -DOAMD_STAMPS"
+s = np.frombuffer(buf, dtype=np.uint64).reshape(wgs, 16).astype(np.int64)
+t0, t1, t2, t3, hw, c1, c2, t7, h0, h1, h2 = (s[:, i] for i in range(11))
 cu_key = ((hw >> 32) << 8) | ((hw >> 8) & 0xFF)  # XCC id, SE/SH/CU fields of HW_ID
 ns = 10.0  # s_memrealtime: 100 MHz
 base = t0.min()
@@ -55,6 +55,9 @@ busy = (pro + tow + hd).sum()
 print(f"rows {rows}: {wgs} workgroups on {len(per_cu)} CUs, launch span {span:.1f} us")
 pin = (t7 - t0) * ns / 1e3
 print(f"prologue split (median us): entry->inputs staged {np.median(pin):.2f}, stage-0 wait + barrier + first reads {np.median(pro - pin):.2f}")
+print(f"heads split (median us): entry {np.median(h0 - t2) * ns / 1e3:.2f}, 1x1 convs (MFMA) "
+      f"{np.median(h1 - h0) * ns / 1e3:.2f}, Linear partials {np.median(h2 - h1) * ns / 1e3:.2f}, "
+      f"softmax/value + stores {np.median(t3 - h2) * ns / 1e3:.2f}")
 print(f"per workgroup (median us): prologue {np.median(pro):.2f}  tower {np.median(tow):.1f}  heads {np.median(hd):.2f}"
       f"  (p90 prologue {np.percentile(pro, 90):.2f}, heads {np.percentile(hd, 90):.2f})")
 print(f"same-CU gap exit->next entry: median {np.median(gaps):.2f} us, p90 {np.percentile(gaps, 90):.2f}, "
