@@ -92,6 +92,11 @@ constexpr int kMaxStampWgs = 1 << 16;
 #ifndef OAMD_ILV
 #define OAMD_ILV 1
 #endif
+// epilogue: wait for the next layer's first weight stage before the first
+// barrier and read its weight fragments during the stores
+#ifndef OAMD_EPI_WEARLY
+#define OAMD_EPI_WEARLY 0  // measured +0.4 % (6 VGPRs spill under the 208 cap)
+#endif
 #ifndef OAMD_VGPR_CAP
 #define OAMD_VGPR_CAP 104  // gfx950 counts the unified VGPR+AGPR file: 2 x 104 = 208
 #endif
@@ -640,6 +645,20 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     const int kg = lane >> 4;
     const int row0 = blockIdx.x * G::BOARDS;
     OAMD_STAMP(0);
+#ifdef OAMD_STAMPS
+    // epilogue cycle sums: first barrier, stores, second barrier + first reads
+    unsigned long long ep_sum[3] = {0, 0, 0}, ep_t = 0;
+#define OAMD_EP_MARK(k)                                                          \
+    do {                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                       \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
+        if ((k) > 0) ep_sum[(k) - 1] += t_ - ep_t;                               \
+        ep_t = t_;                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                       \
+    } while (0)
+#else
+#define OAMD_EP_MARK(k) ((void)0)
+#endif
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
     const int total = (ksteps_first(C) + 2 * N.R * ksteps_tower(C)) / G::KS;
 
@@ -924,13 +943,28 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         // stages g+1 .. (next layer's) are in flight; the next layer's bias is
         // loaded before the next DMA so the counted wait below covers it
         const bool more = layer + 1 < nlayers;
-        if (more) load_bias<G>(bv, N, layer + 1, wn, lane);
+        constexpr bool wearly = OAMD_EPI_WEARLY && !OAMD_REGSTAGE;
+        if constexpr (wearly) {
+            // the next layer's first stage (g + 1) lands before the first
+            // barrier, so its weight fragments are read during the stores
+            if constexpr (!(ABL & 1)) wait_vm<(G::AHEAD - 1) * G::DPT>();
+        } else {
+            if (more) load_bias<G>(bv, N, layer + 1, wn, lane);
+        }
+        OAMD_EP_MARK(0);
         lds_barrier();  // every wave is done reading this layer's input and stage g
+        OAMD_EP_MARK(1);
         if constexpr (OAMD_REGSTAGE) {
             stage_store_lds<G>(stg, ring, (slot + 2) % G::RING, tid);
             stage_load_regs<G>(stg, wsrc, g + 3, total, tid);
         } else {
             issue_stage_dma<G>(wsrc, ring, g + 1 + G::AHEAD, (slot + G::AHEAD + 1) % G::RING, total, tid);
+        }
+        if constexpr (wearly) {
+            if (more) {
+                load_bias<G>(bv, N, layer + 1, wn, lane);
+                load_wfrags<ABL>(fa, ring + (slot == G::RING - 1 ? 0 : slot + 1) * G::STAGE, wl);
+            }
         }
 #pragma unroll
         for (int n = 0; n < kNT; ++n)
@@ -944,11 +978,21 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             }
         ++g;
         slot = slot == G::RING - 1 ? 0 : slot + 1;
+        OAMD_EP_MARK(2);
         if (more) {
-            if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();  // stage g has landed (later may fly)
-            lds_barrier();           // ... and this layer's output is complete
-            load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false), rd, wl);
+            if constexpr (wearly) {
+                lds_barrier();  // this layer's output is complete
+                load_xfrags<ABL>(fa, act, kstep_offset<C>(0, false), rd);
+            } else {
+                if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();  // stage g has landed (later may fly)
+                lds_barrier();           // ... and this layer's output is complete
+                load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false), rd, wl);
+            }
+#ifdef OAMD_STAMPS
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
         }
+        OAMD_EP_MARK(3);
     };
     conv(std::integral_constant<int, 0>{}, 0);
     for (int blk = 0; blk < N.R; ++blk) {
@@ -957,6 +1001,10 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     }
     __syncthreads();  // also drains this wave's trailing ring DMAs: the ring is free
     OAMD_STAMP(2);
+#ifdef OAMD_STAMPS
+    if (wave == 0 && lane == 0 && blockIdx.x < kMaxStampWgs)
+        for (int i = 0; i < 3; ++i) g_oamd_stamps[blockIdx.x * 16 + 11 + i] = ep_sum[i];
+#endif
     if constexpr (ABL & 32) return;
     heads<G, DT>(N, act, ring, wave, lane, row0, rows, policy, value);
     OAMD_STAMP(3);

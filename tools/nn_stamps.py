@@ -30,7 +30,7 @@ wgs = rows // 4
 buf = (ctypes.c_uint64 * (wgs * 16))()
 assert lib.oamd_debug_read_stamps(buf, ctypes.c_int64(wgs * 16)) == 0, "build with -DOAMD_STAMPS"
 s = np.frombuffer(buf, dtype=np.uint64).reshape(wgs, 16).astype(np.int64)
-t0, t1, t2, t3, hw, c1, c2, t7, h0, h1, h2 = (s[:, i] for i in range(11))
+t0, t1, t2, t3, hw, c1, c2, t7, h0, h1, h2, e0, e1, e2 = (s[:, i] for i in range(14))
 cu_key = ((hw >> 32) << 8) | ((hw >> 8) & 0xFF)  # XCC id, SE/SH/CU fields of HW_ID
 ns = 10.0  # s_memrealtime: 100 MHz
 base = t0.min()
@@ -67,4 +67,8 @@ print(f"first entry per CU: median {np.median(first):.2f} us, max {max(first):.2
 print(f"shares of CU time (span x CUs): prologue {pro.sum() / (span * len(per_cu)):.2%}, "
       f"heads {hd.sum() / (span * len(per_cu)):.2%}, tower {tow.sum() / (span * len(per_cu)):.2%}, "
       f"idle {1 - busy / (span * len(per_cu)):.2%}")
+if e0.any():
+    tc = (c2 - c1).astype(float)
+    print(f"epilogues (19 per tower, share of tower cycles, median): first barrier {np.median(e0 / tc):.2%}, "
+          f"stores {np.median(e1 / tc):.2%}, second barrier + next layer's first reads {np.median(e2 / tc):.2%}")
 print(f"tower clock (s_memtime / s_memrealtime): median {np.median(clk):.3f} GHz")
