@@ -28,6 +28,20 @@ FIN_NONE, FIN_DRAW, FIN_BLACK, FIN_WHITE = 0, 1, 2, 3
 _OUTCOME_BLACK = {FIN_DRAW: 0.0, FIN_BLACK: 1.0, FIN_WHITE: -1.0}
 
 
+def outcome_for_black(player1_discs: int, player2_discs: int) -> float:
+    """+1 / -1 / 0 by the final disc count (train.py:438-445)."""
+    b, w = bin(player1_discs).count("1"), bin(player2_discs).count("1")
+    return 1.0 if b > w else (-1.0 if b < w else 0.0)
+
+
+def value_targets_from_outcome(black_to_move: list[bool], player1_discs: int, player2_discs: int) -> list[float]:
+    """One value target per move (the reference repeats it for the move's 8
+    samples): the final outcome from the perspective of the side to move at that
+    step. From the initial position this is train.py:447-450's alternating rule."""
+    v = outcome_for_black(player1_discs, player2_discs)
+    return [v if b else -v for b in black_to_move]
+
+
 class SelfPlayCollector:
     """Accumulates selfplay_move outputs per game; completed games become samples.
 
@@ -99,4 +113,4 @@ def self_play(batched, neural_net, games: int, temperature_moves: int = 12, temp
     return data
 
 
-__all__ = ["SelfPlayCollector", "self_play", "FIN_NONE", "FIN_DRAW", "FIN_BLACK", "FIN_WHITE"]
+__all__ = ["SelfPlayCollector", "self_play", "outcome_for_black", "value_targets_from_outcome", "FIN_NONE", "FIN_DRAW", "FIN_BLACK", "FIN_WHITE"]

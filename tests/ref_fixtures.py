@@ -1,0 +1,100 @@
+"""Loader + replay for the reference-generated MCTS fixtures
+(tests/golden/ref_mcts.*, ref_self_play.*; generator: tests/golden/make_ref_mcts.py,
+which ran the compiled reference extension).
+
+``replay_case`` drives any object with the reference's MCTS surface
+(apply_action / search / visit_counts / mean_action_values / self_play_data /
+position) through one case and compares every move bit for bit with what the
+reference produced. It is shared by the oracle test (CPU) and the HIP test
+(GPU), so both are held to the same reference record.
+"""
+
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def load_cases() -> list[dict]:
+    return json.loads((GOLD / "ref_mcts.json").read_text())["cases"]
+
+
+_arrays = None
+
+
+def arrays():
+    global _arrays
+    if _arrays is None:
+        _arrays = dict(np.load(GOLD / "ref_mcts.npz"))
+    return _arrays
+
+
+def expected(case: dict) -> list[dict]:
+    """Per-move expected records of a case."""
+    a = arrays()
+    name = case["name"]
+    C = 1 + 2 * case["history_size"]
+    offs = np.cumsum([0] + case["num_children"])
+    visits, q = a[f"{name}__visits"], a[f"{name}__q_bits"].view(np.float32)
+    feats = np.unpackbits(a[f"{name}__features_packed"], axis=2)[:, :, : C * 64]
+    out = []
+    for i, act in enumerate(case["actions"]):
+        out.append({
+            "root": case["root_positions"][i],
+            "visits": visits[offs[i]:offs[i + 1]].tolist(),
+            "q": q[offs[i]:offs[i + 1]],
+            "features": feats[i].reshape(8, C, 8, 8).astype(np.float32),
+            "policy": a[f"{name}__policy"][i],
+            "action": act,
+        })
+    return out
+
+
+def replay_case(m, case: dict, search, position_tuple, self_play_data) -> int:
+    """Replay ``case`` on ``m``; returns the number of Q values that differ by
+    more than 0 ulp but within 1e-6 (reported, not failed — SURVEY §4)."""
+    for a in case["prefix"]:
+        m.apply_action(a)
+    ulp_flips = 0
+    for i, exp in enumerate(expected(case)):
+        assert position_tuple(m) == exp["root"], (case["name"], i, "root position")
+        search(m)
+        assert list(m.visit_counts()) == exp["visits"], (case["name"], i)
+        q = np.array(m.mean_action_values(), np.float32)
+        if not np.array_equal(q.view(np.uint32), exp["q"].view(np.uint32)):
+            np.testing.assert_allclose(q, exp["q"], rtol=0, atol=1e-6, err_msg=f"{case['name']} move {i}")
+            ulp_flips += int((q != exp["q"]).sum())
+        f, p = self_play_data(m)
+        np.testing.assert_array_equal(f, exp["features"], err_msg=f"{case['name']} move {i} features")
+        np.testing.assert_array_equal(p, exp["policy"], err_msg=f"{case['name']} move {i} policy")
+        m.apply_action(exp["action"])
+    return ulp_flips
+
+
+def load_self_play() -> tuple[list[dict], dict]:
+    meta = json.loads((GOLD / "ref_self_play.json").read_text())
+    return meta["games"], dict(np.load(GOLD / "ref_self_play.npz"))
+
+
+def self_play_expected(games, arr, gi):
+    g = games[gi]
+    C = g["feature_shape"][0]
+    n = g["samples"]
+    f = np.unpackbits(arr[f"g{gi}__features_packed"], axis=1)[:, : C * 64].reshape(n, C, 8, 8)
+    return f.astype(np.float32), arr[f"g{gi}__policy"], arr[f"g{gi}__values"]
+
+
+def value_targets(num_moves: int, final_p1: int, final_p2: int) -> np.ndarray:
+    """train.py:438-450's rule, restated: +-1/0 by final disc count for step 0,
+    alternating sign per step, 8 samples per step."""
+    b, w = bin(final_p1).count("1"), bin(final_p2).count("1")
+    v = 1.0 if b > w else (-1.0 if b < w else 0.0)
+    out = []
+    for _ in range(num_moves):
+        out += [v] * 8
+        v = -v
+    return np.array(out, np.float32)

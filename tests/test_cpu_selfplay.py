@@ -85,3 +85,37 @@ def test_load_checkpoint_roundtrip_and_validation(tmp_path):
     (d / "config.json").write_text(json.dumps({"neural_net": dict(cfg, conv_channels=256)}))
     with pytest.raises(ValueError, match="conv_channels"):
         load_checkpoint(d)
+
+
+@pytest.mark.parametrize("gi", [0, 1])
+def test_collector_reproduces_reference_self_play_samples(gi):
+    """Feed the reference _self_play game (compiled reference MCTS, tests/golden/
+    ref_self_play.*) to SelfPlayCollector as a selfplay_move stream: the samples
+    it returns are the reference's, in order — features, policies and value
+    targets (train.py:404-452)."""
+    import numpy as np
+
+    import ref_fixtures as RF
+    from othello_mcts import Position
+    from othello_mcts.selfplay import outcome_for_black
+
+    games, arr = RF.load_self_play()
+    g = games[gi]
+    f_exp, p_exp, v_exp = RF.self_play_expected(games, arr, gi)
+    pos = Position.initial_position()
+    for a in g["actions"]:
+        pos = pos.apply_action(a)
+    assert pos.is_terminal()
+    fin = {1.0: FIN_BLACK, -1.0: FIN_WHITE, 0.0: FIN_DRAW}[outcome_for_black(pos.player1_discs(),
+                                                                             pos.player2_discs())]
+    col = SelfPlayCollector(1)
+    n = len(g["actions"])
+    for t, a in enumerate(g["actions"]):
+        out = col.add({"actions": torch.tensor([a], dtype=torch.int32),
+                       "finished": torch.tensor([fin if t == n - 1 else FIN_NONE], dtype=torch.int32),
+                       "features": torch.from_numpy(f_exp[8 * t: 8 * t + 8])[None],
+                       "policy": torch.from_numpy(p_exp[8 * t: 8 * t + 8])[None]})
+    assert len(out["values"]) == 8 * n
+    np.testing.assert_array_equal(torch.stack(out["features"]).numpy(), f_exp)
+    np.testing.assert_array_equal(torch.stack(out["policies"]).numpy(), p_exp)
+    np.testing.assert_array_equal(torch.stack(out["values"]).numpy(), v_exp)

@@ -188,6 +188,69 @@ def test_gpu_mcts_known_answers(om, case):
     assert m.visit_counts() == case["visit_counts"]
 
 
+import ref_fixtures as RF  # noqa: E402
+
+REF_ULP_FLIPS: dict[str, int] = {}
+
+
+def _om_pos(m):
+    p = m.position()
+    return [int(p.player()), f"{p.player1_discs():016x}", f"{p.player2_discs():016x}", f"{p.legal_moves():016x}"]
+
+
+def _om_spd(m):
+    d = m.self_play_data()
+    return torch.stack(d["features"]).numpy(), torch.stack(d["policy"]).numpy()
+
+
+@pytest.mark.parametrize("case", RF.load_cases(), ids=lambda c: c["name"])
+def test_gpu_mcts_matches_reference_matrix(om, case):
+    """HIP search vs the COMPILED REFERENCE (tests/golden/make_ref_mcts.py):
+    every move's visit counts, Q bits, 8-fold features and policies, with tree
+    reuse over the case's fixed action sequence (search_thread.cpp:59-260,
+    mcts.cpp:45-165). Q is allowed 1e-6; ulp flips are reported."""
+    m = _mcts(om, history_size=case["history_size"], num_simulations=case["num_simulations"],
+              num_threads=1, batch_size=case["batch_size"], dirichlet_epsilon=0.0)
+    stub = _torch_stub(O.equivariant_stub if case["stub"] == "equivariant" else O.uniform_stub)
+    flips = RF.replay_case(m, case, lambda mm: mm.search(stub), _om_pos, _om_spd)
+    REF_ULP_FLIPS[case["name"]] = flips
+    print(f"[parity] ref-matrix {case['name']}: moves={len(case['actions'])} q_ulp_flips={flips}")
+
+
+@pytest.mark.parametrize("gi", [0, 1])
+def test_gpu_reproduces_reference_self_play(om, gi):
+    """The reference's train._self_play game (compiled reference MCTS, np.random
+    seeded) replayed through the HIP MCTS drop-in: same per-move 8-fold targets,
+    every chosen action admitted by train.py:421-430's rule, same value targets
+    (train.py:438-450) from othello_mcts.selfplay's outcome rule."""
+    from othello_mcts.selfplay import value_targets_from_outcome
+
+    games, arr = RF.load_self_play()
+    g = games[gi]
+    f_exp, p_exp, v_exp = RF.self_play_expected(games, arr, gi)
+    prm = g["params"]
+    m = _mcts(om, history_size=prm["history_size"], num_simulations=prm["num_simulations"],
+              num_threads=prm["num_threads"], batch_size=prm["batch_size"],
+              dirichlet_epsilon=prm["dirichlet_epsilon"])
+    stub = _torch_stub(O.equivariant_stub)
+    black_to_move = []
+    for t, a in enumerate(g["actions"]):
+        pos = m.position()
+        black_to_move.append(pos.player() == 1)
+        m.search(stub)
+        vc = np.array(m.visit_counts())
+        k = pos.legal_actions().index(a)
+        assert vc[k] > 0 if t < g["temperature_moves"] else vc[k] == vc.max()
+        f, p = _om_spd(m)
+        np.testing.assert_array_equal(f, f_exp[8 * t: 8 * t + 8])
+        np.testing.assert_array_equal(p, p_exp[8 * t: 8 * t + 8])
+        m.apply_action(a)
+    fin = m.position()
+    assert fin.is_terminal()
+    v = value_targets_from_outcome(black_to_move, fin.player1_discs(), fin.player2_discs())
+    np.testing.assert_array_equal(np.repeat(np.array(v, np.float32), 8), v_exp)
+
+
 def _play_vs_oracle(om, moves, **kw):
     m = _mcts(om, **kw)
     ref = O.OracleMCTS(history_size=kw.get("history_size", 4), num_simulations=kw.get("num_simulations", 800),

@@ -180,3 +180,69 @@ def test_resnet_restatement_matches_reference(golden_dir, name):
     out = resnet_ref.forward(sd, torch.from_numpy(g[f"{name}_x"].astype(np.float32)))
     np.testing.assert_allclose(out["policy"].numpy(), g[f"{name}_policy"], atol=2e-6, rtol=1e-4)
     np.testing.assert_allclose(out["value"].numpy(), g[f"{name}_value"], atol=2e-6, rtol=1e-4)
+
+
+# ---------------------------------------------------------------- reference-generated MCTS matrix
+import ref_fixtures as RF  # noqa: E402
+
+
+def _oracle_pos(m):
+    p = m.position()
+    return [int(p.player), f"{p.p1:016x}", f"{p.p2:016x}", f"{p.legal:016x}"]
+
+
+@pytest.mark.parametrize("case", RF.load_cases(), ids=lambda c: c["name"])
+def test_oracle_matches_reference_mcts_matrix(case):
+    """The C restatement vs the COMPILED REFERENCE (make_ref_mcts.py): per move
+    visit counts, Q bits, 8-fold features and policies, tree reuse over >= 10
+    moves (search_thread.cpp:59-260, mcts.cpp:45-165)."""
+    m = O.OracleMCTS(history_size=case["history_size"], num_simulations=case["num_simulations"],
+                     num_threads=1, batch_size=case["batch_size"], dirichlet_epsilon=0.0)
+    stub = O.equivariant_stub if case["stub"] == "equivariant" else O.uniform_stub
+    flips = RF.replay_case(m, case, lambda mm: mm.search(stub), _oracle_pos, lambda mm: mm.self_play_data())
+    assert flips == 0
+
+
+def test_reference_mcts_matrix_shape():
+    """SURVEY §4's matrix is covered: both stubs, B in {1,8,16}, H in {4,8},
+    >= 10 moves per case, a pass among the applied actions."""
+    cases = RF.load_cases()
+    assert len(cases) >= 12
+    assert {c["stub"] for c in cases} == {"equivariant", "uniform"}
+    assert {1, 8, 16} <= {c["batch_size"] for c in cases}
+    assert {4, 8} <= {c["history_size"] for c in cases}
+    assert sum(len(c["actions"]) >= 10 for c in cases) >= 12
+    assert any(64 in c["actions"] for c in cases)
+    assert cases[0]["name"] == "eq_h4_b16_s800_open"
+    assert RF.expected(cases[0])[0]["visits"] == [145, 85, 288, 266]  # SURVEY §4 sample
+
+
+@pytest.mark.parametrize("gi", [0, 1])
+def test_oracle_reproduces_reference_self_play(gi):
+    """The reference's train._self_play on the compiled reference MCTS
+    (train.py:404-452): replaying its actions through the oracle gives the same
+    per-move targets, the sampling rule admits every chosen action, and the
+    value targets follow from the final position."""
+    games, arr = RF.load_self_play()
+    g = games[gi]
+    f_exp, p_exp, v_exp = RF.self_play_expected(games, arr, gi)
+    prm = g["params"]
+    m = O.OracleMCTS(history_size=prm["history_size"], num_simulations=prm["num_simulations"],
+                     num_threads=prm["num_threads"], batch_size=prm["batch_size"],
+                     dirichlet_epsilon=prm["dirichlet_epsilon"])
+    for t, a in enumerate(g["actions"]):
+        m.search(O.equivariant_stub)
+        vc = np.array(m.visit_counts())
+        legal = O.legal_actions(m.position())
+        k = legal.index(a)
+        if t < g["temperature_moves"]:
+            assert vc[k] > 0
+        else:
+            assert vc[k] == vc.max()
+        f, p = m.self_play_data()
+        np.testing.assert_array_equal(f, f_exp[8 * t: 8 * t + 8])
+        np.testing.assert_array_equal(p, p_exp[8 * t: 8 * t + 8])
+        m.apply_action(a)
+    fin = m.position()
+    assert fin.player == 0
+    np.testing.assert_array_equal(RF.value_targets(len(g["actions"]), fin.p1, fin.p2), v_exp)
