@@ -82,9 +82,20 @@ def cpu_baseline(seconds: float, history: int, C: int, R: int, hidden: int) -> d
         moves += 1
     dt = time.perf_counter() - t0
     return {"value": round(sims / dt, 1), "unit": "simulations/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)),
             "sample": f"1 game from the initial position, {moves} moves x 800 sims (T=2 x B=16, "
                       f"eps=0.25), {C}x{R + 1}b fp32 torch-CPU, {dt:.1f} s"}
+
+
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 # ---- multi-GPU plumbing (one process per GPU; games shard, no data-path
@@ -116,6 +127,17 @@ def timed_max(world: int, run, sync, device: str) -> float:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def rank_table(world: int, rank: int, device_id: str, sims: int) -> list[dict]:
+    """[{rank, device, sims}] of every rank (all_gather_object over the job's
+    process group): which physical device each rank ran on and its units."""
+    me = {"rank": rank, "device": device_id, "sims": sims}
+    if world == 1:
+        return [me]
+    out: list = [None] * world
+    dist.all_gather_object(out, me)
+    return out
 
 
 def aggregate_rate(world: int, games: int, sims_per_search: int, steps: int, dt_max: float) -> float:
@@ -192,6 +214,15 @@ def main() -> None:
     ms1, launches1, rows1 = b.engine.nn_timing()
     sel1, bk1, _ = b.engine.tree_timing()
     value = aggregate_rate(world, args.games, sims_per_search, args.steps, dt_max)
+    # every game's search followed the reference: no node pool ran out
+    overflow_games, depth_capped = b.engine.status()
+    if overflow_games or depth_capped:
+        raise SystemExit(f"bench invalid: {overflow_games} game(s) overflowed their node pool, "
+                         f"{depth_capped} hit the depth cap")
+    props = torch.cuda.get_device_properties(local)
+    dev_id = f"{os.uname().nodename}:{getattr(props, 'uuid', local)}"
+    ranks = rank_table(world, rank, dev_id, args.games * sims_per_search * args.steps)
+    n_devices = len({r["device"] for r in ranks})
 
     nn_ms = ms1 - ms0
     nn_launches = launches1 - launches0
@@ -229,8 +260,10 @@ def main() -> None:
                 tree_bytes = {k: v["bytes_per_launch"] for k, v in tj["kernels"].items()}
         except (ValueError, OSError, KeyError):
             tree_bytes = {}
+    # k_tree: one launch per search round and pipeline group; "select" rounds
+    # back up the previous batch and select the next, the final round backs up
     tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch)}
-    for name, ms in (("k_select", sel1 - sel0), ("k_backup", bk1 - bk0)):
+    for name, ms in (("k_tree", sel1 - sel0), ("k_tree_final_backup", bk1 - bk0)):
         avg = ms / max(1, nn_launches)
         entry = {"avg_launch_ms": round(avg, 4)}
         if name in tree_bytes:
@@ -243,7 +276,7 @@ def main() -> None:
         "metric": "MCTS simulations/sec (whole node), 800 sims/move, 128x10b ResNet, 1/2/4/8 GPU",
         "value": round(value, 1),
         "unit": "simulations/s",
-        "n_gpus": world,
+        "n_gpus": n_devices,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt_max * 1e3 / args.steps, 3),
@@ -260,8 +293,13 @@ def main() -> None:
             "games_per_gpu": args.games,
             "sims_per_move": args.sims,
             "leaves_per_step": L,
-            "parallelism": f"games sharded over {world} GPU(s), no collective",
+            "parallelism": (f"games sharded over {world} rank(s) on {n_devices} GPU(s), no collective"
+                            + (" (REHEARSAL: ranks share GPUs; not a scaling point)"
+                               if n_devices < world else "")),
+            "ranks": ranks,
+            "backend": (backend if world > 1 else "none"),
         },
+        "overflow_games": overflow_games,
         "roofline": {
             "bound": "mfma",
             "kernel": "k_resnet_w8 (fused 19-conv tower + heads, 8-wave geometry)",

@@ -173,7 +173,11 @@ int oamd_debug_read_stamps(uint64_t *out, int64_t n);
  * num_threads * batch_size; virtual thread k of a game owns leaves
  * [k*batch_size, (k+1)*batch_size) (search_thread.cpp:59-128).
  *   begin -> steps;  repeat steps times: select, [features, evaluate,
- *   set_evaluation], backup. */
+ *   set_evaluation];  then backup once.
+ * select backs up the previous round's batch of each thread right before that
+ * thread selects its next batch: the interleaving the reference's threads
+ * produce (search_thread.cpp:47-128 with mcts.h:242-251's FIFO NN service).
+ * Calling backup after every select gives the lock-step order instead. */
 int oamd_engine_search_begin(oamd_engine *e, int32_t *steps);
 int oamd_engine_select(oamd_engine *e);
 /* host_out[row] = 1 when the leaf is non-terminal (needs the NN) */
@@ -197,6 +201,11 @@ typedef struct oamd_root_info {
 
 int oamd_engine_root_info(oamd_engine *e, int32_t game, oamd_root_info *info_host,
                           int32_t *visits_host, float *q_host);
+/* Engine health (host outputs; waits for the engine's stream): number of
+ * games whose node pool was exhausted (a leaf could not be expanded: the
+ * search no longer follows the reference) and of games whose descent hit the
+ * path-depth cap, since each game's last reset. Callers raise on nonzero. */
+int oamd_engine_status(oamd_engine *e, int32_t *overflow_games, int32_t *depth_capped_games);
 /* All games at once (device buffers): visits_dev (G, 65) and q_dev (G, 65)
  * indexed BY ACTION (0 where not a child), info_dev (G) */
 int oamd_engine_root_stats(oamd_engine *e, int32_t *visits_dev, float *q_dev,
@@ -226,8 +235,10 @@ typedef struct oamd_selfplay_config {
 } oamd_selfplay_config;
 
 /* Per move, per game outputs (device, may be NULL):
- *   actions_dev (G) chosen action (-1 inactive), finished_dev (G) winner+1
- *   when the game ended this move (1 draw... see DESIGN.md), 0 otherwise;
+ *   actions_dev (G) chosen action (-1 inactive); finished_dev (G): bits 0-1 =
+ *   0 game continues, 1 draw, 2 black won, 3 white won (the game ended with
+ *   this move and restarted); bit 2 = the root was unexpanded, no targets were
+ *   written (the move was uniform); bit 3 = the game's node pool overflowed;
  *   features_dev (G, 8, 1+2H, 8, 8) and policy_dev (G, 8, 65) targets. */
 int oamd_engine_selfplay_move(oamd_engine *e, const oamd_selfplay_config *cfg,
                               int32_t *actions_dev, int32_t *finished_dev, float *features_dev,
@@ -241,9 +252,11 @@ int oamd_engine_game_key(oamd_engine *e, int32_t game, uint64_t *key_host);
  * the launching streams; a query waits for the searches still in flight):
  * total ms spent in the NN kernel, number of NN launches, rows evaluated. */
 int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches, int64_t *rows);
-/* Same for the tree kernels: total ms in k_select and in k_backup (one launch
- * of each per NN launch). Timed searches record 6 HIP events per step and
- * pipeline group on the group's stream. */
+/* Same for the tree kernel (k_tree, one launch per search round and pipeline
+ * group): select_ms = total ms of the rounds that select (each also backs up
+ * the previous batch, thread by thread), backup_ms = total ms of the final
+ * backup-only rounds. launches = NN launches. Timed searches record 4 HIP
+ * events per round and pipeline group on the group's stream. */
 int oamd_engine_tree_timing(const oamd_engine *e, float *select_ms, float *backup_ms, int64_t *launches);
 int oamd_engine_enable_timing(oamd_engine *e, int32_t enable);
 

@@ -490,57 +490,78 @@ static void expand_and_backward(orc_mcts *m, int leaf, int t, const float *polic
     }
 }
 
-/* Lock-step schedule of the reference's T threads x B leaves
- * (search_thread.cpp:47-128, mcts.h:220-256): every step, virtual thread 0
- * selects its B leaves, then thread 1, ... (virtual losses accumulate), then
- * each thread's batch goes through the NN (skipped when all its leaves are
- * terminal, :102), then the threads back up in order. With num_threads = 1 this
- * is exactly the reference; with more threads it is one legal interleaving of
- * the reference's lock/queue protocol. */
+/* One descent of a virtual thread's leaf i (search_thread.cpp:62-79):
+ * PUCT walk to a terminal or unexpanded node, virtual loss on the path below
+ * the root, root N+1, and the leaf's symmetry draw (:92). */
+static void select_leaf(orc_mcts *m, int i) {
+    int node = m->root;
+    while (!(m->nodes[node].pos.player == 0 || m->nodes[node].n_children == 0))
+        node = choose_best_child(m, node);
+    m->leaves[i] = node;
+    for (int x = node; x != m->root; x = m->nodes[x].parent) {
+        onode *c = &m->nodes[x];
+        c->n += 1;
+        c->w -= 1.0f;
+        c->q = c->w / (float)c->n;
+    }
+    m->nodes[m->root].n += 1;
+    if (m->nodes[node].pos.player != 0) {
+        uint64_t ev = m->event++;
+        m->trans[i] = (int32_t)(orc_mix64(orc_stream_key(m->key, ev, 0)) >> 61);
+    } else {
+        m->trans[i] = 0;
+    }
+}
+
+/* Features of thread th's batch and its NN call (search_thread.cpp:84-110;
+ * skipped when every leaf of the batch is terminal, :102). */
+static void evaluate_thread(orc_mcts *m, int th, orc_nn_fn nn, void *user) {
+    int B = m->batch_size, C = m->channels;
+    int any = 0;
+    for (int j = 0; j < B; ++j) {
+        int i = th * B + j;
+        float *f = m->features + (size_t)i * C * 64;
+        if (m->nodes[m->leaves[i]].pos.player == 0) {
+            memset(f, 0, (size_t)C * 64 * sizeof(float));
+            continue;
+        }
+        any = 1;
+        leaf_features(m, m->leaves[i], m->trans[i], f);
+    }
+    if (any)
+        nn(user, m->features + (size_t)th * B * C * 64, B, C, m->policy + (size_t)th * B * 65,
+           m->value + (size_t)th * B);
+}
+
+/* Schedule of the reference's T threads x B leaves (search_thread.cpp:47-128,
+ * mcts.h:220-256). Each thread runs ceil(S / (T*B)) batches of
+ * lock{select B} -> NN round trip -> lock{expand + backup B}; the calling
+ * thread serves NN requests in FIFO order. The interleaving the reference
+ * produces in practice (measured over repeated runs of the compiled
+ * reference, DESIGN.md "Search semantics") is the pipelined round-robin
+ *
+ *     S_0(1) S_1(1) .. S_{T-1}(1)  then, for k = 1..n, for t = 0..T-1:
+ *     B_t(k) S_t(k+1)
+ *
+ * (S = select a batch, B = back it up): a thread whose NN result arrives
+ * backs up and immediately selects its next batch while the NN serves the
+ * next thread. With T = 1 this is exactly the reference's sequential loop. */
 int orc_mcts_search(orc_mcts *m, orc_nn_fn nn, void *user) {
     int T = m->num_threads, B = m->batch_size, L = T * B;
     int steps = (m->num_simulations + L - 1) / L;
-    int C = m->channels;
-    for (int step = 0; step < steps; ++step) {
-        for (int i = 0; i < L; ++i) {
-            int node = m->root;
-            while (!(m->nodes[node].pos.player == 0 || m->nodes[node].n_children == 0))
-                node = choose_best_child(m, node);
-            m->leaves[i] = node;
-            for (int x = node; x != m->root; x = m->nodes[x].parent) {
-                onode *c = &m->nodes[x];
-                c->n += 1;
-                c->w -= 1.0f;
-                c->q = c->w / (float)c->n;
-            }
-            m->nodes[m->root].n += 1;
-            /* transform draw for non-terminal leaves (search_thread.cpp:92) */
-            if (m->nodes[node].pos.player != 0) {
-                uint64_t ev = m->event++;
-                m->trans[i] = (int32_t)(orc_mix64(orc_stream_key(m->key, ev, 0)) >> 61);
-            } else {
-                m->trans[i] = 0;
-            }
-        }
+    for (int round = 0; round <= steps; ++round) {
         for (int th = 0; th < T; ++th) {
-            int any = 0;
-            for (int j = 0; j < B; ++j) {
-                int i = th * B + j;
-                float *f = m->features + (size_t)i * C * 64;
-                if (m->nodes[m->leaves[i]].pos.player == 0) {
-                    memset(f, 0, (size_t)C * 64 * sizeof(float));
-                    continue;
+            if (round > 0)
+                for (int j = 0; j < B; ++j) {
+                    int i = th * B + j;
+                    expand_and_backward(m, m->leaves[i], m->trans[i], m->policy + (size_t)i * 65,
+                                        m->value + i);
                 }
-                any = 1;
-                leaf_features(m, m->leaves[i], m->trans[i], f);
-            }
-            if (any)
-                nn(user, m->features + (size_t)th * B * C * 64, B, C, m->policy + (size_t)th * B * 65,
-                   m->value + (size_t)th * B);
+            if (round < steps)
+                for (int j = 0; j < B; ++j) select_leaf(m, th * B + j);
         }
-        for (int i = 0; i < L; ++i)
-            expand_and_backward(m, m->leaves[i], m->trans[i], m->policy + (size_t)i * 65,
-                                m->value + i);
+        if (round < steps)
+            for (int th = 0; th < T; ++th) evaluate_thread(m, th, nn, user);
     }
     return steps * L;
 }
@@ -608,3 +629,56 @@ int orc_mcts_apply_action(orc_mcts *m, int action) {
 
 int orc_mcts_node_count(const orc_mcts *m) { return m->count; }
 uint64_t orc_mcts_events(const orc_mcts *m) { return m->event; }
+
+/* The self-play move choice of train.py:421-430 as the on-device driver
+ * (tree.hip k_selfplay_move) draws it from one event of the game's stream:
+ * for ply < temperature_moves sample a child with p ~ N^(1/temperature) by a
+ * sequential float cdf (numpy.random.choice's rule); afterwards argmax of N
+ * with a uniform random tie-break; an unexpanded root picks a legal action
+ * uniformly. Returns the action (not applied). */
+int orc_mcts_selfplay_action(orc_mcts *m, int ply, int temperature_moves, float temperature) {
+    const onode *r = &m->nodes[m->root];
+    if (r->pos.player == 0) return -1;
+    int32_t acts[65];
+    orc_pos rp = r->pos;
+    int na = orc_legal_actions(&rp, acts);
+    int nc = r->n_children;
+    uint64_t ev = m->event++;
+    float u = orc_uniform(orc_stream_key(m->key, ev, 0), 0);
+    int j = 0;
+    if (nc == 0) {
+        j = (int)(u * (float)na);
+        if (j >= na) j = na - 1;
+    } else if (ply < temperature_moves) {
+        float cdf[64], sum = 0.0f;
+        for (int k = 0; k < nc; ++k) {
+            sum += powf((float)m->nodes[r->first_child + k].n, 1.0f / temperature);
+            cdf[k] = sum;
+        }
+        if (sum > 0.0f) {
+            float target = u * sum;
+            j = nc - 1;
+            for (int k = 0; k < nc; ++k)
+                if (cdf[k] > target) {
+                    j = k;
+                    break;
+                }
+        } else {
+            j = (int)(u * (float)nc);
+            if (j >= nc) j = nc - 1;
+        }
+    } else {
+        int mx = 0, nt = 0;
+        for (int k = 0; k < nc; ++k)
+            if (m->nodes[r->first_child + k].n > mx) mx = m->nodes[r->first_child + k].n;
+        for (int k = 0; k < nc; ++k) nt += m->nodes[r->first_child + k].n == mx;
+        int pick = (int)(u * (float)nt);
+        if (pick >= nt) pick = nt - 1;
+        for (int k = 0; k < nc; ++k)
+            if (m->nodes[r->first_child + k].n == mx && pick-- == 0) {
+                j = k;
+                break;
+            }
+    }
+    return acts[j];
+}

@@ -96,6 +96,8 @@ int orc_mcts_self_play_data(const orc_mcts *m, float *features, float *policy);
 int orc_mcts_apply_action(orc_mcts *m, int action);
 int orc_mcts_node_count(const orc_mcts *m);
 uint64_t orc_mcts_events(const orc_mcts *m);
+/* train.py:421-430 move choice drawn like the on-device driver (one event) */
+int orc_mcts_selfplay_action(orc_mcts *m, int ply, int temperature_moves, float temperature);
 
 #ifdef __cplusplus
 }

@@ -91,6 +91,7 @@ def lib():
             "orc_mcts_apply_action": (i32, [vp, i32]),
             "orc_mcts_node_count": (i32, [vp]),
             "orc_mcts_events": (u64, [vp]),
+            "orc_mcts_selfplay_action": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_float]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -284,6 +285,10 @@ class OracleMCTS:
 
     def events(self) -> int:
         return lib().orc_mcts_events(self._h)
+
+    def selfplay_action(self, ply: int, temperature_moves: int = 12, temperature: float = 1.0) -> int:
+        """train.py:421-430's choice as the on-device driver draws it (consumes one event)."""
+        return lib().orc_mcts_selfplay_action(self._h, ply, temperature_moves, temperature)
 
 
 # ---------------------------------------------------------------- stub nets

@@ -20,7 +20,7 @@
 using namespace oamd;
 
 constexpr int kMaxPipeline = 8;
-constexpr int kEvPerBlock = 6;  // timing events per (step, group)
+constexpr int kEvPerBlock = 4;  // timing events per (round, group): tree begin/end, NN begin/end
 // NN launches of the pipeline groups run one after another, so each owns every
 // CU while the other groups' tree kernels run beside it and its HIP-event
 // duration is its own. OAMD_NN_ORDER 1: a token event passed between the group
@@ -146,6 +146,7 @@ struct oamd_engine {
     uint8_t* flags = nullptr;
     float* explore_tab = nullptr;
     unsigned long long* counters = nullptr;
+    int32_t* status_dev = nullptr;  // [0] games with pool overflow, [1] depth-capped games
     // query scratch
     oamd_root_info* info_dev = nullptr;
     int32_t* visits_dev = nullptr;
@@ -153,7 +154,7 @@ struct oamd_engine {
     float* spd_dev = nullptr;  // self-play data scratch (8*(1+2H)*64 + 8*65)
     // search state
     int steps_left = 0;
-    int step_phase = 0;  // 0 = expect select, 1 = expect backup
+    int step_phase = 0;  // 1 = a selected round awaits its backup (step API)
     // pipeline groups (0 = auto) and their streams / fork-join events
     int pipeline = 0;
     // rows per k_resnet launch (0 = one launch per group and step); a group's
@@ -172,7 +173,8 @@ struct oamd_engine {
     // summed (waiting for its last event) before reuse or on a timing query
     bool timing = false;
     std::vector<hipEvent_t> ev[2];
-    int ev_blocks[2] = {0, 0};  // pending (step, group) blocks per pool
+    int ev_blocks[2] = {0, 0};  // pending (round, group) blocks per pool
+    int ev_final[2] = {0, 0};   // first block of the backup-only final round
     int64_t ev_launches[2] = {0, 0};  // k_resnet launches inside those blocks
     int64_t ev_rows[2] = {0, 0};
     int ev_cur = 0;
@@ -185,16 +187,19 @@ struct oamd_engine {
     int resolve_timing(int p) {
         const int n = ev_blocks[p];
         if (!n) return OAMD_OK;
-        HIPCHK(hipEventSynchronize(ev[p][kEvPerBlock * n - 1]));
         for (int i = 0; i < n; ++i) {
             const hipEvent_t* b = &ev[p][kEvPerBlock * i];
             float ms = 0.0f;
+            // blocks of different groups end on different streams; the final
+            // round records no NN events
+            HIPCHK(hipEventSynchronize(b[1]));
+            if (i < ev_final[p]) HIPCHK(hipEventSynchronize(b[3]));
             HIPCHK(hipEventElapsedTime(&ms, b[0], b[1]));
-            select_ms += ms;
-            HIPCHK(hipEventElapsedTime(&ms, b[2], b[3]));
-            nn_ms += ms;
-            HIPCHK(hipEventElapsedTime(&ms, b[4], b[5]));
-            backup_ms += ms;
+            (i < ev_final[p] ? select_ms : backup_ms) += ms;
+            if (i < ev_final[p]) {
+                HIPCHK(hipEventElapsedTime(&ms, b[2], b[3]));
+                nn_ms += ms;
+            }
         }
         nn_launches += ev_launches[p];
         nn_rows += ev_rows[p];
@@ -302,6 +307,7 @@ struct oamd_engine {
         dfree(flags);
         dfree(explore_tab);
         dfree(counters);
+        dfree(status_dev);
         dfree(info_dev);
         dfree(visits_dev);
         dfree(q_dev);
@@ -663,7 +669,7 @@ int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity,
     const size_t nodes = (size_t)num_games * node_capacity;
     if ((rc = dalloc(&e->link, nodes)) || (rc = dalloc(&e->stat, nodes)) || (rc = dalloc(&e->pos, nodes)) ||
         (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) || (rc = dalloc(&e->counters, 2)) ||
-        (rc = dalloc(&e->info_dev, num_games)) || (rc = dalloc(&e->visits_dev, (size_t)num_games * 65)) ||
+        (rc = dalloc(&e->status_dev, 2)) || (rc = dalloc(&e->info_dev, num_games)) || (rc = dalloc(&e->visits_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->q_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->spd_dev, (size_t)8 * (1 + 2 * kMaxHistory) * 64 + 8 * 65)) || (rc = e->alloc_rows()) ||
         (rc = e->build_tables())) {
@@ -733,12 +739,15 @@ int oamd_engine_search_begin(oamd_engine* e, int32_t* steps) {
 }
 
 int oamd_engine_select(oamd_engine* e) {
-    if (e->steps_left <= 0 || e->step_phase != 0)
-        return fail(OAMD_INVALID_ARGUMENT, "select called out of order (search_begin / backup first)");
+    if (e->steps_left <= 0)
+        return fail(OAMD_INVALID_ARGUMENT, "select called out of order (search_begin first)");
     DeviceGuard dg(e->device);
-    launch_select(e->view(), e->stream);
+    // a pending round is backed up thread by thread, each thread selecting its
+    // next batch right after its backup (the reference's interleaving, k_tree)
+    launch_tree(e->view(), e->stream, e->step_phase == 1, true, e->cfg.num_threads, e->cfg.batch_size);
     LAUNCHCHK();
     e->step_phase = 1;
+    e->steps_left -= 1;
     return OAMD_OK;
 }
 
@@ -773,10 +782,9 @@ int oamd_engine_set_evaluation(oamd_engine* e, const float* pol, const float* va
 int oamd_engine_backup(oamd_engine* e) {
     if (e->step_phase != 1) return fail(OAMD_INVALID_ARGUMENT, "backup called before select");
     DeviceGuard dg(e->device);
-    launch_backup(e->view(), e->stream);
+    launch_tree(e->view(), e->stream, true, false, e->cfg.num_threads, e->cfg.batch_size);
     LAUNCHCHK();
     e->step_phase = 0;
-    e->steps_left -= 1;
     return OAMD_OK;
 }
 
@@ -823,12 +831,12 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     int rc = e->ensure_streams(K);
     if (rc) return rc;
     if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
-    // timing: per (step, group) kEvPerBlock events: select begin/end, NN
-    // begin/end (on the NN stream, after its waits), backup begin/end
+    // timing: per (round, group) kEvPerBlock events: tree begin/end, NN
+    // begin/end (on the NN stream, after its waits; not in the final round)
     const int pool = e->ev_cur;
     if (e->timing) {
         if ((rc = e->resolve_timing(pool))) return rc;
-        while ((int)e->ev[pool].size() < kEvPerBlock * steps * K) {
+        while ((int)e->ev[pool].size() < kEvPerBlock * (steps + 1) * K) {
             hipEvent_t x;
             HIPCHK(hipEventCreate(&x));
             e->ev[pool].push_back(x);
@@ -845,13 +853,17 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
         HIPCHK(hipEventRecord(e->fork_ev, e->stream));
         for (int k = 0; k < K; ++k) HIPCHK(hipStreamWaitEvent(st[k], e->fork_ev, 0));
     }
-    for (int s = 0; s < steps; ++s) {
+    // rounds 0..steps (k_tree): round s backs up batch s-1 and selects batch s,
+    // thread by thread; the NN evaluates batch s between rounds s and s+1
+    const int T = e->cfg.num_threads, B = e->cfg.batch_size;
+    for (int s = 0; s <= steps; ++s) {
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)g0[k] * L;
             hipEvent_t* ev = e->timing ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
             if (ev) HIPCHK(hipEventRecord(ev[0], st[k]));
-            launch_select(E, st[k], g0[k], ng[k]);
+            launch_tree(E, st[k], s > 0, s < steps, T, B, g0[k], ng[k]);
             if (ev) HIPCHK(hipEventRecord(ev[1], st[k]));
+            if (s == steps) continue;
             // the groups' NN launches run one after another (OAMD_NN_ORDER)
             hipStream_t ns = st[k];
             if (K > 1 && OAMD_NN_ORDER == 2) {
@@ -874,9 +886,6 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             } else if (K > 1 && OAMD_NN_ORDER == 1) {
                 HIPCHK(hipEventRecord(e->nn_token, st[k]));
             }
-            if (ev) HIPCHK(hipEventRecord(ev[4], st[k]));
-            launch_backup(E, st[k], g0[k], ng[k]);
-            if (ev) HIPCHK(hipEventRecord(ev[5], st[k]));
         }
     }
     LAUNCHCHK();
@@ -887,7 +896,8 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
         }
     }
     if (e->timing) {
-        e->ev_blocks[pool] = steps * K;
+        e->ev_blocks[pool] = (steps + 1) * K;
+        e->ev_final[pool] = steps * K;
         int64_t nl = 0;
         for (int k = 0; k < K; ++k) {
             const int grows = ng[k] * L, cb = e->nn_batch > 0 ? e->nn_batch : grows;
@@ -946,6 +956,19 @@ int oamd_engine_root_info(oamd_engine* e, int32_t game, oamd_root_info* info, in
     const int nc = tmp.num_children;
     if (visits) std::memcpy(visits, v, sizeof(int32_t) * nc);
     if (q) std::memcpy(q, qq, sizeof(float) * nc);
+    return OAMD_OK;
+}
+
+int oamd_engine_status(oamd_engine* e, int32_t* overflow_games, int32_t* depth_capped_games) {
+    DeviceGuard dg(e->device);
+    HIPCHK(hipMemsetAsync(e->status_dev, 0, 2 * sizeof(int32_t), e->stream));
+    launch_status(e->view(), e->status_dev, e->stream);
+    LAUNCHCHK();
+    int32_t h[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(h, e->status_dev, sizeof(h), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (overflow_games) *overflow_games = h[0];
+    if (depth_capped_games) *depth_capped_games = h[1];
     return OAMD_OK;
 }
 

@@ -18,9 +18,11 @@ struct SelfplayParams {
 };
 
 // tree.hip
-// games [g0, g0 + ng) (ng < 0: to the end)
-void launch_select(const EngineView& E, hipStream_t s, int g0 = 0, int ng = -1);
-void launch_backup(const EngineView& E, hipStream_t s, int g0 = 0, int ng = -1);
+// One search round for games [g0, g0 + ng) (ng < 0: to the end): for each
+// virtual thread t < T, back up its previous batch (do_backup), then select its
+// next B leaves (do_select). T * B must equal E.L. See tree.hip k_tree.
+void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
+                 int g0 = 0, int ng = -1);
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s);
 void launch_set_evaluation(const EngineView& E, const float* pol, const float* val, int row_begin,
                            int rows, hipStream_t s);
@@ -34,6 +36,7 @@ void launch_self_play_data(const EngineView& E, int g, float* feat, float* pol, 
 void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int32_t* actions,
                           int32_t* finished, float* feat, float* pol, hipStream_t s);
 void launch_random_openings(const EngineView& E, int max_moves, uint64_t seed, hipStream_t s);
+void launch_status(const EngineView& E, int32_t* out, hipStream_t s);
 void launch_legal_moves(const uint64_t* me, const uint64_t* opp, uint64_t* out, int64_t n,
                         hipStream_t s);
 void launch_flips(const uint64_t* mv, const uint64_t* me, const uint64_t* opp, uint64_t* out,

@@ -180,6 +180,19 @@ struct Engine {
         return c;
     }
     void set_config(const oamd_search_config& c) { check(oamd_engine_set_config(h, &c)); }
+    // Raise when a game's node pool ran out (its search stopped following the
+    // reference: leaves could not be expanded) or a descent hit the depth cap.
+    void check_health() const {
+        int32_t over = 0, capped = 0;
+        check(oamd_engine_status(h, &over, &capped));
+        if (over)
+            throw std::runtime_error("node pool exhausted in " + std::to_string(over) +
+                                     " game(s): leaves could not be expanded, so the search no longer "
+                                     "matches the reference; create the engine with a larger node_capacity");
+        if (capped)
+            throw std::runtime_error("search path exceeded the depth cap (127 plies below the root) in " +
+                                     std::to_string(capped) + " game(s)");
+    }
 };
 
 oamd_search_config make_config(int history_size, int num_simulations, int num_threads, int batch_size,
@@ -222,8 +235,9 @@ class MCTS {
 public:
     MCTS(int history_size, std::string torch_device, bool torch_pin_memory, int num_simulations, int num_threads,
          int batch_size, float c_puct_base, float c_puct_init, float dirichlet_epsilon, float dirichlet_alpha,
-         int64_t node_capacity, uint64_t seed)
-        : torch_device_(std::move(torch_device)), pin_(torch_pin_memory) {
+         int64_t node_capacity, uint64_t seed, bool native_nn, const std::string& nn_dtype)
+        : torch_device_(std::move(torch_device)), pin_(torch_pin_memory), native_(native_nn) {
+        set_nn_dtype(nn_dtype);
         const oamd_search_config c = make_config(history_size, num_simulations, num_threads, batch_size,
                                                  c_puct_base, c_puct_init, dirichlet_epsilon, dirichlet_alpha);
         device_ = engine_device_for(torch_device_);
@@ -261,10 +275,11 @@ public:
         check(oamd_engine_set_stream(engine_->h, reinterpret_cast<void*>(stream)));
         const oamd_search_config c = engine_->config();
         if (native_) {
-            py::object nat = T.native.attr("resolve")(neural_net, device_, c.history_size);
+            py::object nat = T.native.attr("resolve")(neural_net, device_, c.history_size, nn_dtype_);
             if (!nat.is_none()) {
                 auto* net = reinterpret_cast<oamd_net*>(nat.attr("handle").cast<uintptr_t>());
                 check(oamd_engine_search(engine_->h, net, nullptr, nullptr));
+                engine_->check_health();
                 return;
             }
         }
@@ -300,9 +315,12 @@ public:
                 check(oamd_engine_set_evaluation(engine_->h, reinterpret_cast<const float*>(T.ptr(pol)),
                                                  reinterpret_cast<const float*>(T.ptr(val)), k * B, B));
             }
-            check(oamd_engine_backup(engine_->h));
         }
+        // the last round's backups (each earlier round was backed up thread by
+        // thread inside the next select, the reference's interleaving)
+        check(oamd_engine_backup(engine_->h));
         sync();
+        engine_->check_health();
     }
 
     // mcts.cpp:45-52
@@ -374,6 +392,12 @@ public:
     // additive API
     bool native_nn() const { return native_; }
     void set_native_nn(bool v) { native_ = v; }
+    std::string nn_dtype() const { return nn_dtype_; }
+    void set_nn_dtype(const std::string& v) {
+        if (v != "bf16" && v != "fp16")
+            throw std::invalid_argument("Expected nn_dtype in {'bf16', 'fp16'}, but got '" + v + "'.");
+        nn_dtype_ = v;
+    }
     int device() const { return device_; }
     uint64_t game_key() {
         uint64_t k = 0;
@@ -411,8 +435,9 @@ private:
 
     std::string torch_device_;
     bool pin_;
-    int device_ = 0;
     bool native_ = true;
+    std::string nn_dtype_ = "bf16";
+    int device_ = 0;
     std::unique_ptr<Engine> engine_;
 };
 
@@ -455,11 +480,12 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
         });
 
     py::class_<MCTS>(m, "MCTS")
-        .def(py::init<int, std::string, bool, int, int, int, float, float, float, float, int64_t, uint64_t>(),
+        .def(py::init<int, std::string, bool, int, int, int, float, float, float, float, int64_t, uint64_t, bool,
+                      const std::string&>(),
              "history_size"_a = 4, "torch_device"_a = "cpu", "torch_pin_memory"_a = false,
              "num_simulations"_a = 800, "num_threads"_a = 2, "batch_size"_a = 16, "c_puct_base"_a = 20000.0f,
              "c_puct_init"_a = 2.5f, "dirichlet_epsilon"_a = 0.25f, "dirichlet_alpha"_a = 0.5f,
-             "node_capacity"_a = 0, "seed"_a = 0)
+             "node_capacity"_a = 0, "seed"_a = 0, "native_nn"_a = true, "nn_dtype"_a = "bf16")
         .def("reset_position", &MCTS::reset_position)
         .def("position", &MCTS::position)
         .def("search", &MCTS::search)
@@ -489,6 +515,8 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
         .def("set_dirichlet_alpha", &MCTS::set_dirichlet_alpha)
         .def("native_nn", &MCTS::native_nn)
         .def("set_native_nn", &MCTS::set_native_nn)
+        .def("nn_dtype", &MCTS::nn_dtype)
+        .def("set_nn_dtype", &MCTS::set_nn_dtype)
         .def("device", &MCTS::device)
         .def("game_key", &MCTS::game_key)
         .def("reset_seed", &MCTS::reset_seed)
@@ -567,6 +595,13 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
                                                   reinterpret_cast<const float*>(val), row_begin, rows));
              })
         .def("backup", [](Engine& e) { check(oamd_engine_backup(e.h)); })
+        .def("status",
+             [](Engine& e) {
+                 int32_t over = 0, capped = 0;
+                 check(oamd_engine_status(e.h, &over, &capped));
+                 return py::make_tuple(over, capped);
+             })
+        .def("check_health", [](Engine& e) { e.check_health(); })
         .def("root_info",
              [](Engine& e, int game) {
                  oamd_root_info info;

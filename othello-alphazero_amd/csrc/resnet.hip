@@ -1016,7 +1016,7 @@ __global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __
     resnet_body<G, DT, IN, ABL>(N, feat_in, fw, H, rows, policy, value);
 }
 // The 8-wave (2 per SIMD) geometry capped at 208 VGPRs: that leaves 96 of a
-// SIMD's 512 for one k_select wave (93 VGPRs, no LDS), so the other pipeline
+// SIMD's 512 for one k_tree wave (<= 96 VGPRs, no LDS), so the other pipeline
 // group's tree kernel co-resides with this kernel instead of waiting for a CU.
 // amdgpu_num_vgpr counts in units of the unified VGPR+AGPR file on gfx950
 // (the backend doubles it), hence OAMD_VGPR_CAP = 104; build.py checks the

@@ -2,10 +2,10 @@
 //
 // The reference runs num_threads CPU threads per game, each selecting
 // batch_size leaves under a mutex with virtual loss, sending them through the
-// NN and backing them up (search_thread.cpp:47-260). Here a whole game's step
-// (L = num_threads * batch_size leaves) is one wave of k_select, one row block
-// of the NN launch, and one wave of k_backup; all games of the engine run in
-// the same launches. Lanes parallelise what is parallel inside one game:
+// NN and backing them up (search_thread.cpp:47-260). Here a round of a game
+// (every thread backs up its previous batch and selects its next one, see
+// k_tree) is one wave of k_tree followed by one row block of the NN launch;
+// all games of the engine run in the same launches. Lanes parallelise what is parallel inside one game:
 // the child scan of PUCT (lane = child), virtual loss and backup (lane = path
 // depth), expansion (lane = square), feature gathers (lane = history slot).
 // The sequential dependence between the L descents (each sees the previous
@@ -188,36 +188,23 @@ __device__ __forceinline__ void write_packed_features(const EngineView& E, size_
 }
 
 // ---------------------------------------------------------------------------
-// Selection: L descents with virtual loss (search_thread.cpp:59-100).
+// Selection: descents i in [i0, i1) with virtual loss (search_thread.cpp:59-100).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_select(EngineView E, int g0) {
-    const int g = g0 + (int)blockIdx.x;
+__device__ __forceinline__ void select_range(const EngineView& E, int g, GameState* gs, size_t base,
+                                             int i0, int i1, uint64_t& event, int hist_node,
+                                             int hist_n, unsigned long long& sims,
+                                             unsigned long long& evals) {
     const int lane = lane_id();
-    GameState* gs = E.games + g;
-    const size_t base = (size_t)g * E.cap;
     const int root = gs->root;
-    const int flags = gs->flags;
     const uint64_t key = gs->key;
-    uint64_t event = gs->event;
-    const int hist_n = gs->hist_n;
-    const int hist_node = lane < 16 ? gs->hist[lane] : -1;
-    unsigned long long sims = 0, evals = 0;
-    // the root's link is fixed during selection (expansions happen in k_backup);
-    // its N grows by one per selected leaf (search_thread.cpp:78)
+    // the root's link is fixed during one thread's selections (expansions happen
+    // in that thread's backup, before this range); its N grows by one per
+    // selected leaf (search_thread.cpp:78)
     const NodeLink root_link = load_link(E.link + base + root);
     int root_n = E.stat[base + root].n;
 
-    for (int i = 0; i < E.L; ++i) {
+    for (int i = i0; i < i1; ++i) {
         const int r = g * E.L + i;
-        if (!(flags & kActive)) {
-            if (lane == 0) {
-                E.leaf[r] = -1;
-                E.depth[r] = 0;
-                E.trans[r] = 0;
-            }
-            write_packed_features(E, base, r, 0, 0, 0, -1, 0, 1, 0, false);
-            continue;
-        }
         int node = root;
         int d = 0;
         int p0 = lane == 0 ? root : -1;  // path slot `lane`
@@ -293,7 +280,7 @@ __global__ __launch_bounds__(64) void k_select(EngineView E, int g0) {
         }
         root_n += 1;
         if (lane == 0) E.stat[base + root].n = root_n;  // search_thread.cpp:78
-        // record the path for the backup kernel
+        // record the path for the backup
         int* gp = E.path + (size_t)r * kMaxDepth;
         if (lane <= d) gp[lane] = p0;
         if (64 + lane <= d) gp[64 + lane] = p1;
@@ -313,36 +300,25 @@ __global__ __launch_bounds__(64) void k_select(EngineView E, int g0) {
         evals += valid ? 1 : 0;
         wait_stores();  // the next descent reads these statistics
     }
-    if (lane == 0) {
-        gs->event = event;
-        if (E.counters) {
-            atomicAdd(E.counters + 0, sims);
-            atomicAdd(E.counters + 1, evals);
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
-// Expansion + backup (search_thread.cpp:116-127, 130-190).
+// Expansion + backup of leaves [i0, i1) (search_thread.cpp:116-127, 130-190).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_backup(EngineView E, int g0) {
-    const int g = g0 + (int)blockIdx.x;
+__device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t base, int i0, int i1,
+                                             int& count, bool& overflow) {
     const int lane = lane_id();
-    GameState* gs = E.games + g;
-    if (!(gs->flags & kActive)) return;
-    const size_t base = (size_t)g * E.cap;
-    int count = gs->count;
-    bool overflow = false;
-    __shared__ int expanded[kMaxLeaves];  // leaves expanded in this step, in order
-    int n_expanded = 0;
-
     // Leaves are processed in order (their backups share path nodes), but
     // everything a leaf needs except the path statistics is independent of
-    // the earlier leaves of the step: it is fetched for 64 leaves at once, one
-    // lane per leaf (a duplicate leaf's link may be stale after its first copy
-    // expanded it; duplicates never expand again and only use the player).
-    for (int c0 = 0; c0 < E.L; c0 += 64) {
-        const int cl = c0 + lane < E.L ? lane : 0;
+    // the earlier leaves: it is fetched for up to 64 leaves at once, one lane
+    // per leaf. A chunk's prefetch starts after every earlier store of the
+    // wave has completed, so links are current except for duplicates of a
+    // leaf expanded earlier in the same chunk: those are found by a ballot
+    // over the chunk's lanes (duplicates never expand again, search_thread.cpp:
+    // 133-135, and use only the immutable player / parent of the link).
+    for (int c0 = i0; c0 < i1; c0 += 64) {
+        const int cend = i1 - c0 < 64 ? i1 - c0 : 64;
+        const int cl = lane < cend ? lane : 0;
         const int rl = g * E.L + c0 + cl;
         const int leaf_v = E.leaf[rl];
         const int d_v = E.depth[rl];
@@ -350,7 +326,7 @@ __global__ __launch_bounds__(64) void k_backup(EngineView E, int g0) {
         const float val_v = E.value[rl];
         const int4 lk_v = *reinterpret_cast<const int4*>(E.link + base + leaf_v);
         const NodePos pos_v = E.pos[base + leaf_v];
-        const int cend = E.L - c0 < 64 ? E.L - c0 : 64;
+        bool expanded_here = false;  // lane j: leaf j of this chunk expanded its node
         // path of the chunk's first leaf; each leaf prefetches the next one's
         int gp0 = 0, gp1 = 0;
         {
@@ -373,10 +349,7 @@ __global__ __launch_bounds__(64) void k_backup(EngineView E, int g0) {
                 if (lane >= 1 && lane <= dn) gp0 = gp[lane];
                 if (64 + lane <= dn) gp1 = gp[64 + lane];
             }
-            // duplicate leaves of one step expand once (search_thread.cpp:133-135)
-            bool hit = false;
-            for (int k = lane; k < n_expanded; k += 64) hit |= expanded[k] == leaf;
-            const bool already = __any(hit);
+            const bool already = __ballot(expanded_here && leaf_v == leaf) != 0;
             if (lk.player != 0 && lk.n_children == 0 && !already) {
                 Pos P;
                 P.player = lk.player;
@@ -412,10 +385,7 @@ __global__ __launch_bounds__(64) void k_backup(EngineView E, int g0) {
                         store_pos(E.pos + base + id, c);
                     }
                     if (lane == 0) store_link(E.link + base + leaf, NodeLink{fc, nc, lk.parent, lk.player});
-                    if (lane == 0) expanded[n_expanded] = leaf;
-                    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS write visible to the wave
-                    __builtin_amdgcn_wave_barrier();
-                    ++n_expanded;
+                    if (lane == j) expanded_here = true;
                 }
             }
             if (d > 0) {
@@ -452,9 +422,68 @@ __global__ __launch_bounds__(64) void k_backup(EngineView E, int g0) {
             wait_stores();  // the next leaf's backup reads these statistics
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// One round of the search schedule for every game (one wave per game).
+//
+// The reference runs T threads, each looping lock{select B leaves} -> NN ->
+// lock{expand + backup B leaves}, with the calling thread serving NN requests
+// FIFO (search_thread.cpp:47-128, mcts.h:220-256). The interleaving it
+// produces (measured on the compiled reference, DESIGN.md "Search semantics")
+// is a pipelined round-robin: after every thread selected its first batch,
+// thread t backs up batch k and immediately selects batch k+1, then thread
+// t+1 does the same. Round k of this kernel is therefore, for t = 0..T-1:
+//     backup(thread t, batch k-1)   [do_backup]
+//     select(thread t, batch k)     [do_select]
+// Thread t's rows are consumed by its backup before its selection rewrites
+// them. With T = 1 this is exactly the reference's sequential loop. Calling
+// with do_backup only after every select gives the lock-step order instead.
+// ---------------------------------------------------------------------------
+// Capped at 96 VGPRs (amdgpu_num_vgpr counts the unified VGPR+AGPR file in
+// units of 2 on gfx950) so that a tree wave fits beside the two 208-VGPR
+// k_resnet_w8 waves of every SIMD (512 VGPRs): one pipeline group's tree round
+// runs on the CUs that the other group's ResNet launch occupies. The cap costs
+// two 8-byte spills outside the descent/backup loops.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree(EngineView E, int g0, int do_backup, int do_select,
+                                             int T, int B) {
+    const int g = g0 + (int)blockIdx.x;
+    const int lane = lane_id();
+    GameState* gs = E.games + g;
+    const size_t base = (size_t)g * E.cap;
+    const int flags = gs->flags;
+    if (!(flags & kActive)) {
+        if (do_select) {
+            for (int i = 0; i < E.L; ++i) {
+                const int r = g * E.L + i;
+                if (lane == 0) {
+                    E.leaf[r] = -1;
+                    E.depth[r] = 0;
+                    E.trans[r] = 0;
+                }
+                write_packed_features(E, base, r, 0, 0, 0, -1, 0, 1, 0, false);
+            }
+        }
+        return;
+    }
+    uint64_t event = gs->event;
+    const int hist_n = gs->hist_n;
+    const int hist_node = lane < 16 ? gs->hist[lane] : -1;
+    unsigned long long sims = 0, evals = 0;
+    int count = gs->count;
+    bool overflow = false;
+    for (int t = 0; t < T; ++t) {
+        if (do_backup) backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
+        if (do_select) select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals);
+    }
     if (lane == 0) {
+        gs->event = event;
         gs->count = count;
         if (overflow) gs->flags |= kOverflow;
+        if (E.counters && do_select) {
+            atomicAdd(E.counters + 0, sims);
+            atomicAdd(E.counters + 1, evals);
+        }
     }
 }
 
@@ -716,6 +745,8 @@ __global__ void k_random_openings(EngineView E, int max_moves, uint64_t seed) {
     random_opening(E, g, max_moves);
 }
 
+constexpr int kFinNoTargets = 4, kFinOverflow = 8;
+
 __global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayParams sp,
                                                       int32_t* actions, int32_t* finished,
                                                       float* feat_out, float* pol_out) {
@@ -734,6 +765,11 @@ __global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayPara
     const NodeLink lk = load_link(E.link + base + root);
     const NodePos rp = E.pos[base + root];
     const int nc = lk.n_children;
+    // status bits reported with `finished` (selfplay.py): the root had no
+    // searched children, so no targets were written (the reference's
+    // self_play_data raises, mcts.cpp:69-71); the game's node pool overflowed
+    const int status = (lk.player != 0 && nc == 0 ? kFinNoTargets : 0) |
+                       (gs->flags & kOverflow ? kFinOverflow : 0);
     int action = -1;
     if (lk.player != 0) {
         const int na = rp.legal ? popcount64(rp.legal) : 1;
@@ -802,8 +838,18 @@ __global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayPara
             random_opening(E, g, sp.opening_moves);
         }
         if (actions) actions[g] = action;
-        if (finished) finished[g] = fin;
+        if (finished) finished[g] = fin | status;
     }
+}
+
+// Games whose node pool overflowed / whose descent hit the depth cap (sticky
+// flags since the game's last reset).
+__global__ void k_status(EngineView E, int32_t* out) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= E.G) return;
+    const int f = E.games[g].flags;
+    if (f & kOverflow) atomicAdd(out + 0, 1);
+    if (f & kDepthCap) atomicAdd(out + 1, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -830,13 +876,12 @@ __global__ void k_apply_positions(const Pos* in, const int32_t* actions, Pos* ou
 // ---------------------------------------------------------------------------
 static inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-void launch_select(const EngineView& E, hipStream_t s, int g0, int ng) {
+void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
+                 int g0, int ng) {
     if (ng < 0) ng = E.G - g0;
-    if (ng > 0) hipLaunchKernelGGL(k_select, dim3(ng), dim3(64), 0, s, E, g0);
-}
-void launch_backup(const EngineView& E, hipStream_t s, int g0, int ng) {
-    if (ng < 0) ng = E.G - g0;
-    if (ng > 0) hipLaunchKernelGGL(k_backup, dim3(ng), dim3(64), 0, s, E, g0);
+    if (T * B != E.L) return;  // caller validated; never launch on a mismatched layout
+    if (ng > 0 && (do_backup || do_select))
+        hipLaunchKernelGGL(k_tree, dim3(ng), dim3(64), 0, s, E, g0, (int)do_backup, (int)do_select, T, B);
 }
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s) {
     if (rows > 0) hipLaunchKernelGGL(k_features_f32, dim3(blocks_for(rows, 4)), dim3(256), 0, s, E, out, row_begin, rows);
@@ -870,6 +915,9 @@ void launch_self_play_data(const EngineView& E, int g, float* feat, float* pol, 
 void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int32_t* actions,
                           int32_t* finished, float* feat, float* pol, hipStream_t s) {
     hipLaunchKernelGGL(k_selfplay_move, dim3(E.G), dim3(64), 0, s, E, sp, actions, finished, feat, pol);
+}
+void launch_status(const EngineView& E, int32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_status, dim3(blocks_for(E.G, 64)), dim3(64), 0, s, E, out);
 }
 void launch_random_openings(const EngineView& E, int max_moves, uint64_t seed, hipStream_t s) {
     hipLaunchKernelGGL(k_random_openings, dim3(blocks_for(E.G, 64)), dim3(64), 0, s, E, max_moves, seed);

@@ -16,6 +16,17 @@ from ._othello_mcts_impl import SearchConfig, _Engine
 from .native import NativeNet, resolve
 
 
+def default_node_capacity(num_simulations: int) -> int:
+    """Power of two >= 64 searches x num_simulations x 12 nodes, in [2^16, 2^22]
+    (observed: ~8.5 children per expansion, games of <= 64 plies; 800 sims ->
+    2^20 nodes = 64 MB per game, 1600 sims -> 2^21)."""
+    need = 64 * max(1, num_simulations) * 12
+    cap = 1 << 16
+    while cap < need and cap < (1 << 22):
+        cap <<= 1
+    return cap
+
+
 class BatchedMCTS:
     def __init__(
         self,
@@ -32,11 +43,17 @@ class BatchedMCTS:
         seed: int = 0,
         node_capacity: int = 0,
     ) -> None:
+        """node_capacity: nodes per game (0 = sized from num_simulations: a whole
+        game of 64 searches at ~12 new nodes per simulation, 2^16..2^22). Nodes are
+        reclaimed when a game restarts; running out raises (check_health)."""
         if device is None:
             device = torch.cuda.current_device()
         self.device = torch.device("cuda", device)
         self.config = SearchConfig(history_size, num_simulations, num_threads, batch_size, c_puct_base,
                                    c_puct_init, dirichlet_epsilon, dirichlet_alpha)
+        if node_capacity == 0:
+            node_capacity = default_node_capacity(num_simulations)
+        self.node_capacity = node_capacity
         self.engine = _Engine(device, num_games, node_capacity, self.config, seed)
         self.num_games = num_games
         self._actions = torch.empty(num_games, dtype=torch.int32, device=self.device)
@@ -64,22 +81,39 @@ class BatchedMCTS:
         self._stream()
         nat = resolve(neural_net, self.device.index, self.config.history_size)
         if nat is not None:
-            return self.engine.search(nat.handle, sync)
-        # external evaluator: one call per step over all G * L rows
+            r = self.engine.search(nat.handle, sync)
+            if sync:
+                self.engine.check_health()  # raises if a node pool ran out
+            return r
+        # external evaluator: one call per step over all G * L rows. Each select
+        # backs up the previous round thread by thread (the reference's
+        # interleaving, csrc/tree.hip k_tree); one backup closes the search.
         rows = self.rows_per_step
         feat = torch.empty((rows, self._C, 8, 8), dtype=torch.float32, device=self.device)
         steps = self.engine.search_begin()
         sims = evals = 0
         for _ in range(steps):
             self.engine.select()
+            # leaf flags: 1 = non-terminal leaf (an NN row); terminal leaves are
+            # simulations without an evaluation (search_thread.cpp:88-90)
+            flags = self.engine.leaf_flags()
             self.engine.features(feat.data_ptr(), 0, rows)
             out = neural_net(feat)
             pol = out["policy"].detach().to(self.device, torch.float32).contiguous()
             val = out["value"].detach().to(self.device, torch.float32).contiguous()
             self.engine.set_evaluation(pol.data_ptr(), val.data_ptr(), 0, rows)
-            self.engine.backup()
-            sims += rows
+            evals += int(flags.sum())
+            sims += rows  # every game of the engine is active (k_tree)
+        self.engine.backup()
+        self.engine.check_health()
         return sims, evals
+
+    def check_health(self) -> None:
+        """Raise RuntimeError if any game's node pool ran out or a descent hit
+        the depth cap (waits for the engine's stream). Asynchronous searches
+        (sync=False) are checked here or by SelfPlayCollector."""
+        self._stream()
+        self.engine.check_health()
 
     def reset(self, game: int = -1, seed: int = 0) -> None:
         self._stream()

@@ -13,14 +13,19 @@ no Python in the loop.
 converted once and cached; the cache is invalidated whenever a parameter or
 buffer is modified in place (tensor ``_version``), so a training loop that
 updates the net between self-play games is always searched with fresh
-weights. Set ``OTHELLO_MCTS_NATIVE_NN=0`` (or ``MCTS.set_native_nn(False)``)
-to always call the Python module instead (the reference's exact numerics).
+weights. The switch from the module's fp32 forward to the native kernel's
+bf16 (``MCTS(nn_dtype=...)``: "bf16" default, "fp16") is announced by a
+one-time RuntimeWarning; only a module whose forward is the stock
+AlphaZeroNet.forward is replaced. Set ``OTHELLO_MCTS_NATIVE_NN=0`` (or
+``MCTS(native_nn=False)`` / ``set_native_nn(False)``) to always call the Python
+module instead (the reference's exact numerics).
 """
 
 from __future__ import annotations
 
 import json
 import os
+import warnings
 import weakref
 from pathlib import Path
 
@@ -123,7 +128,31 @@ class NativeNet:
 
 
 def _looks_like_alphazero(m) -> bool:
-    return all(hasattr(m, a) for a in ("conv_block", "residual_blocks", "policy_head", "value_head"))
+    """An AlphaZeroNet (neural_net.py:138-172) whose forward is the stock one: a
+    subclass that overrides forward (logits, temperature, ...) is never
+    replaced by the native kernel, which computes the stock forward."""
+    if not all(hasattr(m, a) for a in ("conv_block", "residual_blocks", "policy_head", "value_head")):
+        return False
+    for cls in type(m).__mro__:
+        if "forward" in vars(cls):
+            return cls.__name__ == "AlphaZeroNet"
+    return False
+
+
+_warned: set = set()
+
+
+def _warn_once(m, dtype: str) -> None:
+    key = (id(type(m)), dtype)
+    if key in _warned:
+        return
+    _warned.add(key)
+    warnings.warn(
+        f"othello_mcts: evaluating {type(m).__name__} with the native fused kernel in {dtype} "
+        "(the reference calls the module's own fp32 forward); near-tied visit counts can differ. "
+        "MCTS(..., native_nn=False) / set_native_nn(False) or OTHELLO_MCTS_NATIVE_NN=0 keeps the "
+        "module's forward; nn_dtype='fp16' is the closer native precision.",
+        RuntimeWarning, stacklevel=3)
 
 
 _cache: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
@@ -136,8 +165,12 @@ def _signature(m) -> tuple:
     return tuple(sig)
 
 
-def resolve(neural_net, device: int, history_size: int):
-    """NativeNet to use for ``neural_net`` on ``device``, or None (call it instead)."""
+def resolve(neural_net, device: int, history_size: int, dtype: str = "bf16"):
+    """NativeNet to use for ``neural_net`` on ``device``, or None (call it instead).
+
+    A NativeNet is used as given. A stock AlphaZeroNet module in eval mode is
+    converted once to a NativeNet of ``dtype`` (cached until a parameter or
+    buffer changes) and a one-time RuntimeWarning names the precision switch."""
     if isinstance(neural_net, NativeNet):
         if neural_net.device.index != device:
             raise ValueError(f"NativeNet lives on cuda:{neural_net.device.index}, the search on cuda:{device}")
@@ -146,6 +179,8 @@ def resolve(neural_net, device: int, history_size: int):
         return neural_net
     if os.environ.get("OTHELLO_MCTS_NATIVE_NN", "1") == "0":
         return None
+    if dtype not in _DTYPES:
+        raise ValueError(f"nn_dtype must be one of {sorted(_DTYPES)}, got {dtype!r}")
     m = getattr(neural_net, "_orig_mod", neural_net)
     if not isinstance(m, torch.nn.Module) or not _looks_like_alphazero(m) or m.training:
         return None
@@ -159,8 +194,9 @@ def resolve(neural_net, device: int, history_size: int):
         return None
     sig = _signature(m)
     hit = _cache.get(m)
-    if hit is not None and hit[0] == sig and hit[1].device.index == device:
+    if hit is not None and hit[0] == sig and hit[1].device.index == device and hit[1].dtype == dtype:
         return hit[1]
-    nn_ = NativeNet(m, device=device)
+    _warn_once(m, dtype)
+    nn_ = NativeNet(m, device=device, dtype=dtype)
     _cache[m] = (sig, nn_)
     return nn_

@@ -23,8 +23,11 @@ from __future__ import annotations
 
 import torch
 
-# BatchedMCTS.selfplay_move "finished" codes (csrc/tree.hip k_selfplay_move)
+# BatchedMCTS.selfplay_move "finished" codes (csrc/tree.hip k_selfplay_move):
+# bits 0-1 outcome of a game that ended with this move, bit 2 no targets were
+# written (unexpanded root), bit 3 the game's node pool overflowed
 FIN_NONE, FIN_DRAW, FIN_BLACK, FIN_WHITE = 0, 1, 2, 3
+FIN_NO_TARGETS, FIN_OVERFLOW = 4, 8
 _OUTCOME_BLACK = {FIN_DRAW: 0.0, FIN_BLACK: 1.0, FIN_WHITE: -1.0}
 
 
@@ -67,10 +70,18 @@ class SelfPlayCollector:
         # the output buffers are reused by the next move: copy this move's targets
         feats = out["features"].to(self.device, copy=True)
         pols = out["policy"].to(self.device, copy=True)
+        bad = (finished & FIN_OVERFLOW) != 0
+        if bool(bad.any()):
+            raise RuntimeError(f"node pool exhausted in game(s) {bad.nonzero().flatten().tolist()}: the search no "
+                               "longer matches the reference; use a larger node_capacity")
+        no_targets = (finished & FIN_NO_TARGETS) != 0
+        if bool((no_targets & (actions >= 0)).any()):
+            # the reference's self_play_data raises here (mcts.cpp:69-71)
+            raise ValueError("The root node has not been expanded yet.")
         for g in range(self.num_games):
             if int(actions[g]) >= 0:  # a searched, expanded root: targets were written
                 self._moves[g].append((feats[g], pols[g]))
-            fin = int(finished[g])
+            fin = int(finished[g]) & 3
             if fin != FIN_NONE:
                 self._finish(g, _OUTCOME_BLACK[fin])
         return self.drain()
@@ -113,4 +124,5 @@ def self_play(batched, neural_net, games: int, temperature_moves: int = 12, temp
     return data
 
 
-__all__ = ["SelfPlayCollector", "self_play", "outcome_for_black", "value_targets_from_outcome", "FIN_NONE", "FIN_DRAW", "FIN_BLACK", "FIN_WHITE"]
+__all__ = ["SelfPlayCollector", "self_play", "outcome_for_black", "value_targets_from_outcome",
+           "FIN_NO_TARGETS", "FIN_OVERFLOW", "FIN_NONE", "FIN_DRAW", "FIN_BLACK", "FIN_WHITE"]

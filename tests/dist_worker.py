@@ -44,8 +44,11 @@ def main() -> None:
     shards = [None] * world
     dist.all_gather_object(shards, {"rank": rank, "local": local, "seeds": [engine_seed, opening_seed],
                                     "dt_max": dt_max, "played": played})
+    # which device each rank ran on (here: one CPU "device" per local rank)
+    ranks = bench.rank_table(world, rank, f"cpu{local}", games * sims)
     if rank == 0:
-        print(json.dumps({"world": world, "rate": rate, "dt_max": dt_max, "shards": shards}), flush=True)
+        print(json.dumps({"world": world, "rate": rate, "dt_max": dt_max, "shards": shards,
+                          "ranks": ranks}), flush=True)
     dist.destroy_process_group()
 
 

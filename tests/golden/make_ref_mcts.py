@@ -109,33 +109,50 @@ def pos_tuple(p) -> list:
 
 
 # ---------------------------------------------------------------- known-answer matrix
-def run_case(om, case: dict, arrays: dict) -> None:
+def _run_once(om, case: dict) -> dict:
     m = om.MCTS(history_size=case["history_size"], num_simulations=case["num_simulations"],
-                num_threads=1, batch_size=case["batch_size"], dirichlet_epsilon=0.0)
+                num_threads=case["num_threads"], batch_size=case["batch_size"], dirichlet_epsilon=0.0)
     for a in case["prefix"]:
         m.apply_action(a)
     stub = STUBS[case["stub"]]
-    visits, q, feats, pols, roots = [], [], [], [], []
+    rec = {"visits": [], "q": [], "feats": [], "pols": [], "roots": []}
     for a in case["actions"]:
-        roots.append(pos_tuple(m.position()))
+        rec["roots"].append(pos_tuple(m.position()))
         m.search(stub)
-        vc = m.visit_counts()
-        visits.append(vc)
-        q.append(np.array(m.mean_action_values(), np.float32))
+        rec["visits"].append(m.visit_counts())
+        rec["q"].append(np.array(m.mean_action_values(), np.float32))
         d = m.self_play_data()
         f = torch.stack(d["features"]).numpy()
         assert set(np.unique(f)) <= {0.0, 1.0}
-        feats.append(np.packbits(f.astype(np.uint8).reshape(8, -1), axis=1))
-        pols.append(torch.stack(d["policy"]).numpy().astype(np.float32))
+        rec["feats"].append(np.packbits(f.astype(np.uint8).reshape(8, -1), axis=1))
+        rec["pols"].append(torch.stack(d["policy"]).numpy().astype(np.float32))
         m.apply_action(a)
-    case["root_positions"] = roots
-    case["num_children"] = [len(v) for v in visits]
+    return rec
+
+
+def _key(rec: dict) -> tuple:
+    return tuple(tuple(v) for v in rec["visits"]) + tuple(q.tobytes() for q in rec["q"])
+
+
+def run_case(om, case: dict, arrays: dict) -> None:
+    """num_threads = 1: one run (the reference is deterministic there). With
+    more threads the reference's interleaving is racy: the case is run
+    `repeats` times and the modal trajectory is recorded with its frequency."""
+    runs = [_run_once(om, case) for _ in range(case.get("repeats", 1))]
+    keys = [_key(r) for r in runs]
+    modal = max(set(keys), key=keys.count)
+    rec = runs[keys.index(modal)]
+    if case.get("repeats", 1) > 1:
+        case["modal_runs"] = keys.count(modal)
+    case["root_positions"] = rec["roots"]
+    case["num_children"] = [len(v) for v in rec["visits"]]
     name = case["name"]
-    arrays[f"{name}__visits"] = np.concatenate([np.array(v, np.int32) for v in visits])
-    arrays[f"{name}__q_bits"] = np.concatenate(q).view(np.uint32)
-    arrays[f"{name}__features_packed"] = np.stack(feats)
-    arrays[f"{name}__policy"] = np.stack(pols)
-    print(f"{name}: {len(visits)} moves, root visits move 0 {visits[0]}")
+    arrays[f"{name}__visits"] = np.concatenate([np.array(v, np.int32) for v in rec["visits"]])
+    arrays[f"{name}__q_bits"] = np.concatenate(rec["q"]).view(np.uint32)
+    arrays[f"{name}__features_packed"] = np.stack(rec["feats"])
+    arrays[f"{name}__policy"] = np.stack(rec["pols"])
+    extra = f" (modal {case['modal_runs']}/{case['repeats']})" if "modal_runs" in case else ""
+    print(f"{name}: {len(rec['visits'])} moves, root visits move 0 {rec['visits'][0]}{extra}")
 
 
 def make_matrix(om) -> None:
@@ -144,11 +161,11 @@ def make_matrix(om) -> None:
     win = lambda lo, n: (acts[:lo], acts[lo:lo + n])  # noqa: E731
     cases = []
 
-    def add(name, stub, H, B, S, lo, n):
+    def add(name, stub, H, B, S, lo, n, T=1, repeats=1):
         prefix, seq = win(lo, n)
         cases.append({"name": name, "stub": stub, "history_size": H, "batch_size": B,
-                      "num_threads": 1, "num_simulations": S, "dirichlet_epsilon": 0.0,
-                      "prefix": prefix, "actions": seq})
+                      "num_threads": T, "num_simulations": S, "dirichlet_epsilon": 0.0,
+                      "prefix": prefix, "actions": seq, "repeats": repeats})
 
     lo = max(0, pass_ply - 6)
     # the SURVEY sample (H=4, B=16, 800 sims from the initial position) and its continuation
@@ -167,9 +184,16 @@ def make_matrix(om) -> None:
     # through to the end of the game: terminal leaves and the last plies
     add("eq_h4_b16_s160_end", "equivariant", 4, 16, 160, len(acts) - 12, 12)
     add("uni_h8_b8_s64_end", "uniform", 8, 8, 64, len(acts) - 10, 10)
+    # several search threads: the reference's racy interleaving, modal trajectory
+    # of repeated runs (the self-play default T=2 x B=16 at H=8 first)
+    add("eq_h8_t2_b16_s800_open", "equivariant", 8, 16, 800, 0, 6, T=2, repeats=10)
+    add("eq_h4_t2_b8_s160_pass", "equivariant", 4, 8, 160, lo, 10, T=2, repeats=10)
+    add("uni_h4_t2_b16_s320_mid", "uniform", 4, 16, 320, 20, 8, T=2, repeats=10)
+    add("eq_h4_t3_b4_s200_open", "equivariant", 4, 4, 200, 0, 8, T=3, repeats=10)
+    add("eq_h4_t4_b8_s256_pass", "equivariant", 4, 8, 256, lo, 2, T=4, repeats=20)
     # the survey's root-batch quirk case (after actions 19, 18)
     cases.append({"name": "uni_h3_b8_s64_quirk", "stub": "uniform", "history_size": 3, "batch_size": 8,
-                  "num_threads": 1, "num_simulations": 64, "dirichlet_epsilon": 0.0,
+                  "num_threads": 1, "num_simulations": 64, "dirichlet_epsilon": 0.0, "repeats": 1,
                   "prefix": [19, 18], "actions": acts[2:3] if acts[:2] == [19, 18] else [int(
                       om.Position.initial_position().apply_action(19).apply_action(18).legal_actions()[0])]})
     arrays: dict[str, np.ndarray] = {}

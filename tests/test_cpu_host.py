@@ -193,3 +193,42 @@ def test_resnet_activation_layout_is_bank_conflict_free():
                             addrs = [(b * 100 + pad_row(tile[m][lane & 15]) + shift) * pitch
                                      + (kc * 4 + chunk(lane >> 4)) * 16 for lane in g]
                             assert len({(a // 16) % 16 for a in addrs}) == 16
+
+
+def test_type_stub_covers_the_reference_surface_and_the_module():
+    """The .pyi lists every name the compiled module exports, and every
+    function/method of the reference's stub (_othello_mcts_impl.pyi:1-74,
+    recorded here as names) with the same parameter names."""
+    import ast
+    from pathlib import Path
+
+    import othello_mcts._othello_mcts_impl as impl
+
+    stub = Path(impl.__file__).with_name("_othello_mcts_impl.pyi")
+    tree = ast.parse(stub.read_text())
+    names = {n.name for n in tree.body if isinstance(n, (ast.FunctionDef, ast.ClassDef))}
+    exported = {k for k in dir(impl) if not k.startswith("__")}
+    assert exported <= names, exported - names
+    classes = {n.name: n for n in tree.body if isinstance(n, ast.ClassDef)}
+
+    def params(cls, meth):
+        for f in classes[cls].body:
+            if isinstance(f, ast.FunctionDef) and f.name == meth:
+                return [a.arg for a in f.args.posonlyargs + f.args.args]
+        raise AssertionError(f"{cls}.{meth} missing from the stub")
+
+    ref_mcts = ["reset_position", "position", "search", "visit_counts", "mean_action_values", "self_play_data",
+                "apply_action"] + [p + n for n in ("history_size", "torch_device", "torch_pin_memory",
+                                                   "num_simulations", "num_threads", "batch_size", "c_puct_base",
+                                                   "c_puct_init", "dirichlet_epsilon", "dirichlet_alpha")
+                                   for p in ("", "set_")]
+    for m in ref_mcts:
+        params("MCTS", m)
+        assert hasattr(impl.MCTS, m)
+    assert params("MCTS", "__init__")[:11] == ["self", "history_size", "torch_device", "torch_pin_memory",
+                                               "num_simulations", "num_threads", "batch_size", "c_puct_base",
+                                               "c_puct_init", "dirichlet_epsilon", "dirichlet_alpha"]
+    for m in ("initial_position", "player", "player1_discs", "player2_discs", "__getitem__", "legal_moves",
+              "legal_actions", "apply_move", "apply_pass", "apply_action", "is_terminal", "__str__"):
+        params("Position", m)
+        assert hasattr(impl.Position, m)

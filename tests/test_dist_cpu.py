@@ -38,6 +38,10 @@ def test_two_rank_gloo_bench_plumbing():
     assert shards[0]["seeds"] != shards[1]["seeds"]
     assert shards[0]["played"] != shards[1]["played"]
     assert all(0 < sum(v) <= 32 for s in shards for v in s["played"])
+    # the rank table names every rank's device and units (bench.py's n_gpus =
+    # distinct devices, so ranks sharing a GPU are not counted twice)
+    assert [r["rank"] for r in out["ranks"]] == [0, 1]
+    assert len({r["device"] for r in out["ranks"]}) == 2 and all(r["sims"] == 64 for r in out["ranks"])
 
 
 def test_single_rank_helpers():

@@ -210,7 +210,7 @@ def test_gpu_mcts_matches_reference_matrix(om, case):
     reuse over the case's fixed action sequence (search_thread.cpp:59-260,
     mcts.cpp:45-165). Q is allowed 1e-6; ulp flips are reported."""
     m = _mcts(om, history_size=case["history_size"], num_simulations=case["num_simulations"],
-              num_threads=1, batch_size=case["batch_size"], dirichlet_epsilon=0.0)
+              num_threads=case["num_threads"], batch_size=case["batch_size"], dirichlet_epsilon=0.0)
     stub = _torch_stub(O.equivariant_stub if case["stub"] == "equivariant" else O.uniform_stub)
     flips = RF.replay_case(m, case, lambda mm: mm.search(stub), _om_pos, _om_spd)
     REF_ULP_FLIPS[case["name"]] = flips

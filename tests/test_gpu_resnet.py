@@ -4,7 +4,8 @@ Yardsticks: the reference's own AlphaZeroNet outputs (tests/golden/resnet.npz,
 fp32 torch CPU) and the fp32 torch restatement (oracle/resnet_ref.py) on the
 same inputs. The kernel computes in bf16 (or fp16) with fp32 accumulation and
 fp32 heads; tolerances (absolute, on probabilities / tanh values):
-  bf16: policy <= 2e-3, value <= 3e-2;  fp16: policy <= 5e-4, value <= 6e-3.
+  bf16: policy <= 2e-3, value <= 1e-2;  fp16: policy <= 5e-4, value <= 2e-3.
+Every case's measured maxima are printed in the terminal summary (numerics.py).
 """
 
 import json
@@ -13,12 +14,13 @@ import numpy as np
 import pytest
 import torch
 
+import numerics
 import resnet_ref
 
 pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda", 0)
-TOL = {"bf16": (2e-3, 3e-2), "fp16": (5e-4, 6e-3)}
+TOL = {"bf16": (2e-3, 1e-2), "fp16": (5e-4, 2e-3)}
 
 
 @pytest.fixture(scope="module")
@@ -46,7 +48,7 @@ def test_native_net_vs_reference_golden(om, golden_dir, name, dtype):
     torch.cuda.synchronize()
     dp = np.abs(out["policy"].cpu().numpy() - g[f"{name}_policy"]).max()
     dv = np.abs(out["value"].cpu().numpy() - g[f"{name}_value"]).max()
-    print(f"{name} {dtype}: max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e}")
+    numerics.record(f"resnet golden {name} {dtype}", f"max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e}")
     tp, tv = TOL[dtype]
     assert dp <= tp and dv <= tv
 
@@ -67,7 +69,7 @@ def test_native_net_vs_torch_fp32_restatement(om, rows, dtype):
     out = net(x)
     dp = (out["policy"] - ref["policy"]).abs().max().item()
     dv = (out["value"] - ref["value"]).abs().max().item()
-    print(f"rows={rows} {dtype}: max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e}")
+    numerics.record(f"resnet restatement rows={rows} {dtype}", f"max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e}")
     tp, tv = TOL[dtype]
     assert dp <= tp and dv <= tv
     torch.testing.assert_close(out["policy"].sum(1), torch.ones(rows, device=DEV), atol=1e-5, rtol=0)
@@ -87,6 +89,9 @@ def test_native_net_max_history_vs_restatement(om, dtype):
     ref = resnet_ref.forward(sd, x)
     out = net(x)
     tp, tv = TOL[dtype]
+    numerics.record(f"resnet history15 {dtype}",
+                    f"max|dpolicy|={(out['policy'] - ref['policy']).abs().max().item():.2e} "
+                    f"max|dvalue|={(out['value'] - ref['value']).abs().max().item():.2e}")
     assert (out["policy"] - ref["policy"]).abs().max().item() <= tp
     assert (out["value"] - ref["value"]).abs().max().item() <= tv
 
@@ -128,7 +133,7 @@ def test_mcts_autodetects_alphazero_module(om):
 
     sd = alphazero_state_dict(8, 9, 128, 1, 32)
 
-    class Mod(torch.nn.Module):
+    class AlphaZeroNet(torch.nn.Module):  # stands in for neural_net.py:138-172 (stock forward)
         def __init__(self):
             super().__init__()
             self.conv_block = torch.nn.Module()
@@ -141,9 +146,20 @@ def test_mcts_autodetects_alphazero_module(om):
         def state_dict(self, *a, **k):
             return dict(self._sd)
 
-    m = Mod().eval()
-    nn1 = native.resolve(m, 0, 4)
+        def forward(self, x):
+            raise AssertionError("replaced by the native kernel")
+
+    class LogitsNet(AlphaZeroNet):  # overrides forward: never replaced
+        def forward(self, x):
+            return {}
+
+    m = AlphaZeroNet().eval()
+    with pytest.warns(RuntimeWarning, match="bf16"):
+        nn1 = native.resolve(m, 0, 4)
     assert nn1 is not None and native.resolve(m, 0, 4) is nn1
+    assert native.resolve(LogitsNet().eval(), 0, 4) is None
+    nn16 = native.resolve(m, 0, 4, "fp16")
+    assert nn16 is not None and nn16.dtype == "fp16"
 
 
 def test_pipeline_groups_do_not_change_results(om):

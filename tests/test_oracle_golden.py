@@ -197,7 +197,7 @@ def test_oracle_matches_reference_mcts_matrix(case):
     visit counts, Q bits, 8-fold features and policies, tree reuse over >= 10
     moves (search_thread.cpp:59-260, mcts.cpp:45-165)."""
     m = O.OracleMCTS(history_size=case["history_size"], num_simulations=case["num_simulations"],
-                     num_threads=1, batch_size=case["batch_size"], dirichlet_epsilon=0.0)
+                     num_threads=case["num_threads"], batch_size=case["batch_size"], dirichlet_epsilon=0.0)
     stub = O.equivariant_stub if case["stub"] == "equivariant" else O.uniform_stub
     flips = RF.replay_case(m, case, lambda mm: mm.search(stub), _oracle_pos, lambda mm: mm.self_play_data())
     assert flips == 0

@@ -57,7 +57,7 @@ def main(tag: str) -> None:
             "rows_per_launch": bench_line["roofline"]["rows_per_launch"] if bench_line else None,
             "note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> B), rocprofv3 --pmc, separate passes"}, indent=1))
     tree = {}
-    for name in ("k_select", "k_backup"):
+    for name in ("k_tree",):
         k = kern.get(name, {})
         if "FETCH_SIZE_per_launch" in k and "WRITE_SIZE_per_launch" in k:
             tree[name] = {"bytes_per_launch": round(2.0 * k["FETCH_SIZE_per_launch"] * 1024

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters of the tree kernels in the single-game latency run (one wave per
-# kernel): where a k_select / k_backup wave spends its cycles.
+# kernel): where a k_tree wave spends its cycles.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -15,7 +15,7 @@ acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob("gpurun_out/tpmc/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].split()[-1]
-        if "k_select" in k or "k_backup" in k:
+        if "k_tree" in k:
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in acc.items():
     print(k, {c: round(sum(v) / len(v)) for c, v in sorted(cs.items())})
