@@ -50,9 +50,13 @@ def resnet_flops_per_eval(in_ch: int, C: int, R: int, hidden: int) -> float:
     return float(conv0 + tower + heads)
 
 
-def cpu_baseline(seconds: float, history: int, C: int, R: int, hidden: int) -> dict:
+def cpu_baseline(seconds: float, history: int, C: int, R: int, hidden: int, max_moves: int | None = None,
+                 warmup_moves: int = 0) -> dict:
     """Oracle port of the reference CPU path (configs[0]): 1 game, 2 threads x 16,
-    800 sims/move, fp32 torch-CPU ResNet; moves until `seconds` elapse."""
+    800 sims/move, fp32 torch-CPU ResNet; moves until `seconds` elapse (or
+    `max_moves`), after `warmup_moves` untimed moves. Validated against the
+    compiled reference in the build container: tools/cpu_baseline_validate.py,
+    profiles/r02_cpu_baseline_validation.json."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
 
@@ -70,15 +74,21 @@ def cpu_baseline(seconds: float, history: int, C: int, R: int, hidden: int) -> d
 
     m = O.OracleMCTS(history_size=history, num_simulations=800, num_threads=2, batch_size=16,
                      dirichlet_epsilon=0.25, game_key=5)
+    def move():
+        if m.position().player == 0:
+            m.reset_position()
+        n = m.search(nn)
+        vc = m.visit_counts()
+        m.apply_action(O.legal_actions(m.position())[int(np.argmax(vc))])
+        return n
+
+    for _ in range(warmup_moves):
+        move()
     sims = 0
     moves = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        if m.position().player == 0:
-            m.reset_position()
-        sims += m.search(nn)
-        vc = m.visit_counts()
-        m.apply_action(O.legal_actions(m.position())[int(np.argmax(vc))])
+    while time.perf_counter() - t0 < seconds and (max_moves is None or moves < max_moves):
+        sims += move()
         moves += 1
     dt = time.perf_counter() - t0
     return {"value": round(sims / dt, 1), "unit": "simulations/s", "cores": torch.get_num_threads(),
