@@ -113,6 +113,40 @@ constexpr int kMaxStampWgs = 1 << 16;
 #define OAMD_REGSTAGE 0
 #endif
 static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the per-step lgkmcnt(0) fence");
+// Who issues a stage's LDS-DMA pieces (throughput geometry at C=128: 8 waves,
+// 2 pieces per wave and stage, 2 K-steps per stage; other geometries use 0):
+//   0  every wave issues its 2 pieces at the stage-opening barrier
+//   1  every wave issues 1 piece at the opening step and 1 at the stage's
+//      second K-step (the two partners of a SIMD never stall in DMA issue for
+//      a whole step together)
+//   2  alternating halves: waves 0-3 issue all pieces of even stages, waves
+//      4-7 of odd stages (4 each), so one wave of every SIMD pair issues MFMAs
+//      while its partner issues DMA
+//   3  both pieces at the stage's second K-step: no DMA issue between the
+//      stage barrier and the weight-fragment reads behind it
+#ifndef OAMD_DMA_MODE
+#define OAMD_DMA_MODE 1  // same box, 4096 rows: 0.887-0.901 vs 0.909-0.921 ms (mode 0), bit-identical
+#endif
+// modes 1/3: pin the second K-step's DMA issue after this many of its
+// fragment reads (0 = leave the placement to the scheduler)
+#ifndef OAMD_DMA_PIN
+#define OAMD_DMA_PIN 0
+#endif
+// s_setprio 1 for waves 4-7 (the SIMD partners dispatched second) for the
+// whole tower, no per-segment flips (MI355X_MICROARCH.md, two waves per SIMD 4)
+#ifndef OAMD_PRIO_STATIC
+#define OAMD_PRIO_STATIC 0
+#endif
+// Early stage opening (throughput geometry at C=128): the barrier that opens
+// stage g+1 moves from the step that loads g+1's first K-step to the step
+// that loads stage g's second K-step, behind that step's fragment reads. The
+// weight reads of a new stage then never wait on a barrier, and the DMA issued
+// at the barrier refills stage g-1's slot with stage g+2 (two steps of lead).
+// 1 = the whole stage is issued at the barrier, 2 = its second piece at the
+// next step.
+#ifndef OAMD_EARLY_OPEN
+#define OAMD_EARLY_OPEN 0
+#endif
 #ifndef OAMD_STAGGER
 #define OAMD_STAGGER 0
 #endif
@@ -220,8 +254,22 @@ struct GeoT {
     // lgkmcnt(0) fence), so s-1's slot is free and AHEAD = RING - 1 stages fly
     // while one is read (OAMD_DEEP_DMA=0: RING - 2, no reliance on the fence).
     static constexpr int AHEAD = OAMD_DEEP_DMA ? RING - 1 : RING - 2;
-    static constexpr int VM_OPEN = (AHEAD - 1) * DPT;  // vmcnt at a stage-opening barrier
-    static constexpr int VM_LAYER = AHEAD * DPT;       // vmcnt after an epilogue's extra issue
+    static constexpr bool EARLY = OAMD_EARLY_OPEN && WAVES == 8 && KS == 2 && DPT == 2 && RING == 3 &&
+                                  !OAMD_REGSTAGE && !OAMD_STAGGER && OAMD_DEEP_DMA;
+    static constexpr bool EARLY_SPLIT = EARLY && OAMD_EARLY_OPEN == 2;
+    static constexpr int DMA_MODE = (WAVES == 8 && KS == 2 && DPT == 2 && !OAMD_REGSTAGE && !EARLY) ? OAMD_DMA_MODE : 0;
+    // vmcnt at a stage-opening barrier (mode 2: for the half that issued the
+    // stage being opened; the other half need not wait, VM_OPEN_OTHER)
+    static constexpr int VM_OPEN = DMA_MODE == 2 ? 0 : (AHEAD - 1) * DPT;
+    static constexpr int VM_OPEN_OTHER = DMA_MODE == 2 ? 2 * DPT : VM_OPEN;
+    // vmcnt after an epilogue's (or the prologue's) extra issue: mode 1 has
+    // issued only the first piece of the newest stage
+    static constexpr int VM_LAYER = DMA_MODE == 1 ? AHEAD * DPT - 1 : (DMA_MODE == 3 ? (AHEAD - 1) * DPT : AHEAD * DPT);
+    // what an opening (prologue, epilogue, stage barrier) issues of stage
+    // s + AHEAD: -1 all of this wave's pieces, 0 the first, -2 nothing (the
+    // stage's second K-step issues the rest)
+    static constexpr int OPEN_PART = DMA_MODE == 1 ? 0 : (DMA_MODE == 3 ? -2 : -1);
+    static constexpr int MID_PART = DMA_MODE == 1 ? 1 : -1;  // modes 1 and 3 only
     static_assert(RING >= (OAMD_REGSTAGE ? 2 : 3) && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
     static_assert(ksteps_first(C) % KS == 0 && ksteps_tower(C) % KS == 0, "whole stages per layer");
     static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 63, "decomposition");
@@ -367,16 +415,31 @@ __device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[NT][4], const Frags<NT
 
 // Stages past the last one re-read the last stage into a slot nobody reads any
 // more: the issue stays branch-free and the vmcnt bookkeeping uniform.
-template <class G>
+// PART: -1 = all of this wave's pieces of stage g; 0 / 1 = its first / second
+// piece (DMA_MODE 1). DMA_MODE 2: only the half owning stage g issues, 2 x DPT
+// pieces per wave.
+template <class G, int PART = -1>
 __device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsigned char* ring, int g, int slot,
                                                 int total, int tid) {
     const unsigned char* src = wsrc + (size_t)(g < total ? g : total - 1) * G::STAGE;
     unsigned char* dst = ring + slot * G::STAGE;
     const int wave = tid >> 6, lane = tid & 63;
+    if constexpr (PART == -2) {
+        return;
+    } else if constexpr (G::DMA_MODE == 2) {
+        if ((g & 1) != (wave >> 2)) return;  // wave-uniform
 #pragma unroll
-    for (int i = 0; i < G::DPT; ++i) {
-        const int q = i * G::THREADS + wave * 64;  // first 16-byte chunk of this wave's piece
-        __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
+        for (int i = 0; i < 2 * G::DPT; ++i) {
+            const int q = (i * 4 + (wave & 3)) * 64;  // 1 KiB piece i*4 + wave%4
+            __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < G::DPT; ++i) {
+            if (PART >= 0 && i != PART) continue;
+            const int q = i * G::THREADS + wave * 64;  // first 16-byte chunk of this wave's piece
+            __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
+        }
     }
 }
 
@@ -672,8 +735,16 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         stage_store_lds<G>(stg, ring, 1 % G::RING, tid);
         stage_load_regs<G>(stg, wsrc, 2, total, tid);
     } else {
+        if constexpr (G::EARLY) {
+            // stages 0 and 1; stage 2 goes out at stage 0's barrier
+            issue_stage_dma<G>(wsrc, ring, 0, 0, total, tid);
+            issue_stage_dma<G>(wsrc, ring, 1, 1, total, tid);
+        } else {
 #pragma unroll
-        for (int s = 0; s <= G::AHEAD; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
+            for (int s = 0; s < G::AHEAD; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
+            // mode 1: the newest stage's second piece goes out at stage 0's second K-step
+            issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, G::AHEAD, G::AHEAD, total, tid);
+        }
     }
 
     float4 bv[kNT];  // folded bias of this lane's output channels (current layer)
@@ -764,10 +835,13 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 
     OAMD_STAMP(7);
     // stage 0 and the input planes must be visible (bias loads are older than the DMAs)
-    if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();
+    if constexpr (G::EARLY) wait_vm<G::DPT>();  // stage 0 landed (over-waits for stage 1: once)
+    else if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();
     lds_barrier();
     load_frags(fa, act, ring, kstep_offset<C>(0, true), rd, wl);
     OAMD_STAMP(1);
+    if constexpr (OAMD_PRIO_STATIC && G::WAVES == 8)
+        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 
     const int nlayers = 1 + 2 * N.R;
     // one conv layer: KIND 0 = first conv, 1 = a block's first conv (saves the
@@ -817,16 +891,51 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 mfma_half<DT>(acc, cur, 0);
                 __builtin_amdgcn_sched_barrier(0);
             }
+            if constexpr (G::EARLY) {
+                if constexpr (open) {
+                    // first K-step of stage g+1, opened by the previous step's barrier
+                    ++g;
+                    slot = slot == G::RING - 1 ? 0 : slot + 1;
+                    if constexpr (G::EARLY_SPLIT && !(ABL & 8)) {
+                        const int sa = slot == G::RING - 1 ? 0 : slot + 1;
+                        issue_stage_dma<G, 1>(wsrc, ring, g + 1, sa, total, tid);
+                    }
+                    load_wfrags<ABL>(nxt, ring + slot * G::STAGE, wl);
+                    load_xfrags<ABL>(nxt, act, xoff, rd);
+                } else {
+                    // second K-step of stage g: its reads first, then the barrier
+                    // that opens stage g+1 (every wave's DMA of it has landed, and
+                    // every wave has retired its reads of stage g-1)
+                    load_xfrags<ABL>(nxt, act, xoff, rd);
+                    load_wfrags<ABL>(nxt, ring + slot * G::STAGE + G::KSTEP_BYTES, wl);
+                    if constexpr (!(ABL & 1)) {
+                        wait_vm<0>();
+                        __builtin_amdgcn_s_barrier();
+                    }
+                    if constexpr (!(ABL & 8)) {
+                        int sa = slot + 2;
+                        sa = sa >= G::RING ? sa - G::RING : sa;
+                        issue_stage_dma<G, G::EARLY_SPLIT ? 0 : -1>(wsrc, ring, g + 2, sa, total, tid);
+                    }
+                }
+            }
             // activation fragments do not depend on the stage barrier (the
             // layer's input is fixed): with OAMD_XEARLY they are issued before
             // it, so their latency overlaps the barrier wait
-            if constexpr (OAMD_XEARLY) load_xfrags<ABL>(nxt, act, xoff, rd);
+            if constexpr (OAMD_XEARLY && !G::EARLY) load_xfrags<ABL>(nxt, act, xoff, rd);
             int sp = 0;
-            if constexpr (open) {
+            if constexpr (open && !G::EARLY) {
                 // open stage g+1: it has landed (this wave's DMAs, then everyone's
                 // via the barrier) and stage g-1's slot is drained by all waves
                 if constexpr (!(ABL & 1)) {
-                    if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_OPEN>();
+                    if constexpr (G::DMA_MODE == 2) {
+                        // the half that issued stage g+1 waits for it; the other
+                        // half has only stage g+2 in flight
+                        if (((g + 1) & 1) == (wave >> 2)) wait_vm<G::VM_OPEN>();
+                        else wait_vm<G::VM_OPEN_OTHER>();
+                    } else if constexpr (!OAMD_REGSTAGE) {
+                        wait_vm<G::VM_OPEN>();
+                    }
                     __builtin_amdgcn_s_barrier();
                 }
                 sp = (slot + G::AHEAD + 1) % G::RING;  // (g + 1 + AHEAD) % RING
@@ -835,14 +944,20 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     stage_store_lds<G>(stg, ring, (slot + 2) % G::RING, tid);
                     stage_load_regs<G>(stg, wsrc, g + 3, total, tid);
                 } else if constexpr (!(ABL & 8) && !OAMD_DMA_LATE) {
-                    issue_stage_dma<G>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
+                    issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
                 }
                 ++g;
                 slot = slot == G::RING - 1 ? 0 : slot + 1;
+            } else if constexpr ((G::DMA_MODE == 1 || G::DMA_MODE == 3) && !(ABL & 8) && !G::EARLY) {
+                // the rest of stage g + AHEAD (its slot, stage g-1's, was freed
+                // by the barrier that opened stage g)
+                int sa = slot + G::AHEAD;
+                sa = sa >= G::RING ? sa - G::RING : sa;
+                issue_stage_dma<G, G::MID_PART>(wsrc, ring, g + G::AHEAD, sa, total, tid);
             }
             constexpr int kis = open ? 0 : 1;  // K-step within its stage
-            load_wfrags<ABL>(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
-            if constexpr (!OAMD_XEARLY) load_xfrags<ABL>(nxt, act, xoff, rd);
+            if constexpr (!G::EARLY) load_wfrags<ABL>(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
+            if constexpr (!OAMD_XEARLY && !G::EARLY) load_xfrags<ABL>(nxt, act, xoff, rd);
             if constexpr (open && !(ABL & 8) && OAMD_DMA_LATE)
                 issue_stage_dma<G>(wsrc, ring, g + G::AHEAD, sp, total, tid);
             if constexpr (gb) {
@@ -866,14 +981,17 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             // stage-opening step has the 4 weight reads after the barrier (the
             // activation reads precede it, OAMD_XEARLY), the other step all 8
             if constexpr (!gb) {
-                constexpr int nds = open && OAMD_XEARLY ? 4 : 8;
+                constexpr int nds = open && OAMD_XEARLY && !G::EARLY ? 4 : 8;
                 if constexpr (OAMD_ILV == 2 && open) __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
                 if constexpr (OAMD_ILV == 5 && open) {  // DMA after the first read + 4 MFMAs
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     __builtin_amdgcn_sched_group_barrier(0x008, 16 / nds, 0);
                     __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
                 }
-                static_for<(OAMD_ILV == 4 ? nds / 2 : (OAMD_ILV == 5 && open ? nds - 1 : nds))>([&](auto) {
+                static_for<(OAMD_ILV == 4 ? nds / 2 : (OAMD_ILV == 5 && open ? nds - 1 : nds))>([&](auto I) {
+                    if constexpr (!open && OAMD_DMA_PIN > 0 && decltype(I)::value == OAMD_DMA_PIN &&
+                                  (G::DMA_MODE == 1 || G::DMA_MODE == 3))
+                        __builtin_amdgcn_sched_group_barrier(0x020, G::DMA_MODE == 1 ? 1 : G::DPT, 0);
                     if constexpr (OAMD_ILV == 4) {
                         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                         __builtin_amdgcn_sched_group_barrier(0x008, 32 / nds, 0);
@@ -954,11 +1072,20 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         OAMD_EP_MARK(0);
         lds_barrier();  // every wave is done reading this layer's input and stage g
         OAMD_EP_MARK(1);
-        if constexpr (OAMD_REGSTAGE) {
+        if constexpr (G::EARLY) {
+            // stage g+1 was opened by the layer's last barrier; with the split
+            // issue, the second piece of stage g+2 goes out here
+            if constexpr (G::EARLY_SPLIT && !(ABL & 8)) {
+                int sa = slot + 2;
+                sa = sa >= G::RING ? sa - G::RING : sa;
+                issue_stage_dma<G, 1>(wsrc, ring, g + 2, sa, total, tid);
+            }
+        } else if constexpr (OAMD_REGSTAGE) {
             stage_store_lds<G>(stg, ring, (slot + 2) % G::RING, tid);
             stage_load_regs<G>(stg, wsrc, g + 3, total, tid);
         } else {
-            issue_stage_dma<G>(wsrc, ring, g + 1 + G::AHEAD, (slot + G::AHEAD + 1) % G::RING, total, tid);
+            issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, (slot + G::AHEAD + 1) % G::RING, total,
+                                             tid);
         }
         if constexpr (wearly) {
             if (more) {
@@ -984,7 +1111,9 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 lds_barrier();  // this layer's output is complete
                 load_xfrags<ABL>(fa, act, kstep_offset<C>(0, false), rd);
             } else {
-                if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();  // stage g has landed (later may fly)
+                // stage g has landed (later may fly); with EARLY the last barrier
+                // of the layer already waited for it
+                if constexpr (!OAMD_REGSTAGE && !G::EARLY) wait_vm<G::VM_LAYER>();
                 lds_barrier();           // ... and this layer's output is complete
                 load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false), rd, wl);
             }
@@ -1000,6 +1129,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         conv(std::integral_constant<int, 2>{}, 2 + 2 * blk);
     }
     __syncthreads();  // also drains this wave's trailing ring DMAs: the ring is free
+    if constexpr (OAMD_PRIO_STATIC && G::WAVES == 8) __builtin_amdgcn_s_setprio(0);
     OAMD_STAMP(2);
 #ifdef OAMD_STAMPS
     if (wave == 0 && lane == 0 && blockIdx.x < kMaxStampWgs)

@@ -19,7 +19,7 @@ C = int(os.environ.get("NN_C", "128"))  # 128 -> 128x10b, 256 -> 256x20b
 R = 9 if C == 128 else 19
 net = om.NativeNet(alphazero_state_dict(1, 17, C, R, C), device=0)
 flops = 2.0 * 64 * 9 * C * (17 + 2 * R * C) + 2.0 * (64 * C * 3 + 128 * 65 + 64 * C + C)  # bench.py
-x = (torch.rand((rows, 17, 8, 8), device="cuda") < 0.3).float()
+x = (torch.rand((rows, 17, 8, 8), generator=torch.Generator().manual_seed(7)) < 0.3).float().cuda()
 for _ in range(3):
     net(x)
 torch.cuda.synchronize()
@@ -34,4 +34,26 @@ for _ in range(5):
     ms.append(a.elapsed_time(b) / 10)
 ms.sort()
 t = ms[len(ms) // 2]
-print(f"variant {v}: {t:.3f} ms/launch  {flops * rows / t / 1e9:.1f} TFLOP/s  (rows={rows})", flush=True)
+# schedule variants must not change a bit: compare with the saved reference
+out = net(x)
+torch.cuda.synchronize()
+chk = ""
+ref_file = os.environ.get("AB_REF")
+if ref_file:
+    # variants that change the K order (OAMD_KPERM) have their own reference;
+    # every variant is also compared with the first (baseline) reference
+    base_file = ref_file
+    if "OAMD_KPERM=1" in os.environ.get("AB_FLAGS", ""):
+        ref_file = ref_file + ".kperm"
+    if not os.path.exists(ref_file):
+        torch.save({k: t_.cpu() for k, t_ in out.items()}, ref_file)
+        chk = " [saved reference outputs]"
+    else:
+        ref = torch.load(ref_file, weights_only=True)
+        same = all(torch.equal(ref[k], out[k].cpu()) for k in ref)
+        chk = " [outputs bit-identical]" if same else " [OUTPUTS DIFFER]"
+    if ref_file != base_file and os.path.exists(base_file):
+        b = torch.load(base_file, weights_only=True)
+        chk += (f" [vs baseline max|dp|={(b['policy'] - out['policy'].cpu()).abs().max().item():.2e}"
+                f" max|dv|={(b['value'] - out['value'].cpu()).abs().max().item():.2e}]")
+print(f"variant {v}: {t:.3f} ms/launch  {flops * rows / t / 1e9:.1f} TFLOP/s  (rows={rows}){chk}", flush=True)
