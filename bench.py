@@ -175,6 +175,9 @@ def main() -> None:
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
+    ap.add_argument("--timing-every", type=int, default=5,
+                    help="record the kernels' HIP events on every N-th timed search (1 = all; the event "
+                         "packets add ~10 us per NN launch boundary to the searches they time)")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -212,7 +215,7 @@ def main() -> None:
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    b.engine.enable_timing(True)
+    b.engine.enable_timing(max(1, args.timing_every))
     ms0, launches0, rows0 = b.engine.nn_timing()
     sel0, bk0, _ = b.engine.tree_timing()
 

@@ -258,6 +258,8 @@ int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches,
  * backup-only rounds. launches = NN launches. Timed searches record 4 HIP
  * events per round and pipeline group on the group's stream. */
 int oamd_engine_tree_timing(const oamd_engine *e, float *select_ms, float *backup_ms, int64_t *launches);
+/* enable: 0 off, 1 time every search, N >= 2 time every N-th search (sampled:
+ * a timed search's event packets lengthen the gaps between its launches). */
 int oamd_engine_enable_timing(oamd_engine *e, int32_t enable);
 
 #ifdef __cplusplus

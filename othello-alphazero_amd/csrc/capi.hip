@@ -172,6 +172,8 @@ struct oamd_engine {
     // turn, so a search never waits for the previous one's events; a pool is
     // summed (waiting for its last event) before reuse or on a timing query
     bool timing = false;
+    int timing_stride = 1;     // time every timing_stride-th search (sampled timing)
+    int64_t search_count = 0;
     std::vector<hipEvent_t> ev[2];
     int ev_blocks[2] = {0, 0};  // pending (round, group) blocks per pool
     int ev_final[2] = {0, 0};   // first block of the backup-only final round
@@ -789,7 +791,10 @@ int oamd_engine_backup(oamd_engine* e) {
 }
 
 int oamd_engine_enable_timing(oamd_engine* e, int32_t enable) {
+    if (enable < 0) return fail(OAMD_INVALID_ARGUMENT, "enable_timing: expected >= 0");
     e->timing = enable != 0;
+    e->timing_stride = enable > 1 ? enable : 1;
+    e->search_count = 0;
     return OAMD_OK;
 }
 
@@ -831,10 +836,12 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     int rc = e->ensure_streams(K);
     if (rc) return rc;
     if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
+    // sampled timing: every timing_stride-th search records its events
+    const bool timed = e->timing && (e->search_count++ % e->timing_stride) == 0;
     // timing: per (round, group) kEvPerBlock events: tree begin/end, NN
     // begin/end (on the NN stream, after its waits; not in the final round)
     const int pool = e->ev_cur;
-    if (e->timing) {
+    if (timed) {
         if ((rc = e->resolve_timing(pool))) return rc;
         while ((int)e->ev[pool].size() < kEvPerBlock * (steps + 1) * K) {
             hipEvent_t x;
@@ -859,7 +866,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     for (int s = 0; s <= steps; ++s) {
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)g0[k] * L;
-            hipEvent_t* ev = e->timing ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
+            hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
             if (ev) HIPCHK(hipEventRecord(ev[0], st[k]));
             launch_tree(E, st[k], s > 0, s < steps, T, B, g0[k], ng[k]);
             if (ev) HIPCHK(hipEventRecord(ev[1], st[k]));
@@ -895,7 +902,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             HIPCHK(hipStreamWaitEvent(e->stream, e->join_ev[k], 0));
         }
     }
-    if (e->timing) {
+    if (timed) {
         e->ev_blocks[pool] = (steps + 1) * K;
         e->ev_final[pool] = steps * K;
         int64_t nl = 0;

@@ -652,7 +652,8 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
                  check(oamd_engine_game_key(e.h, game, &k));
                  return k;
              })
-        .def("enable_timing", [](Engine& e, bool on) { check(oamd_engine_enable_timing(e.h, on ? 1 : 0)); })
+        .def("enable_timing", [](Engine& e, int every) { check(oamd_engine_enable_timing(e.h, every)); },
+             py::arg("every") = 1)
         .def("set_pipeline", [](Engine& e, int groups) { check(oamd_engine_set_pipeline(e.h, groups)); })
         .def("set_nn_batch", [](Engine& e, int rows) { check(oamd_engine_set_nn_batch(e.h, rows)); })
         .def("nn_timing", [](Engine& e) {
