@@ -164,7 +164,8 @@ void orc_features(const orc_pos *chain, int n_chain, int history_size, int t, fl
 
 /* ======================================================================= */
 /* Random streams — DESIGN.md "Random streams". Replaces the reference's    */
-/* std::mt19937 + std::gamma_distribution (search_thread.cpp:22-24,113-115) */
+/* std::mt19937 + std::gamma_distribution (search_thread.h:77-79,         */
+/* search_thread.cpp:22-24, draws at :92 and :233)                          */
 /* ======================================================================= */
 
 #define GOLDEN 0x9E3779B97F4A7C15ULL
