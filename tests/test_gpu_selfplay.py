@@ -209,3 +209,60 @@ def test_collector_rejects_unexpanded_roots():
     assert ((out["finished"].cpu() & FIN_NO_TARGETS) != 0).all()
     with pytest.raises(ValueError, match="The root node has not been expanded yet."):
         SelfPlayCollector(4).add(out)
+
+
+def test_device_sample_buffer_training_and_refresh():
+    """self-play samples stay in HBM (SampleBuffer == the host
+    collector's samples), a training epoch runs on them on the device, and the
+    trained weights reach the engine's NativeNet (refresh_native == a fresh
+    NativeNet of those weights, bit for bit)."""
+    import othello_mcts as om
+    from othello_mcts.selfplay import SelfPlayCollector
+    from othello_mcts.synthetic import alphazero_state_dict
+    from othello_mcts.training import SampleBuffer, refresh_native, train_epoch
+
+    G = 16
+    net = om.NativeNet(alphazero_state_dict(4, 5, 128, 1, 32), device=0)
+    b = om.BatchedMCTS(G, history_size=2, num_simulations=16, num_threads=1, batch_size=8, seed=3,
+                       node_capacity=1 << 14)
+    col = SelfPlayCollector(G, device=DEV)
+    buf = SampleBuffer(G, 5, capacity=1 << 14, device=DEV)
+    ref = {"features": [], "policies": [], "values": []}
+    while col.games_completed < G:
+        b.search(net)
+        out = b.selfplay_move(emit_targets=True)
+        buf.add(out)
+        got = col.add(out)
+        for k in ref:
+            ref[k] += got[k]
+    assert buf.games_completed == col.games_completed and buf.size == len(ref["values"])
+    assert torch.equal(buf.features[:buf.size], torch.stack(ref["features"]))
+    assert torch.equal(buf.policies[:buf.size], torch.stack(ref["policies"]))
+    assert torch.equal(buf.values[:buf.size], torch.stack(ref["values"]))
+
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = torch.nn.Linear(5 * 64, 66)
+
+        def forward(self, x):
+            y = self.lin(x.flatten(1))
+            return {"policy": torch.softmax(y[:, :65], 1), "value": torch.tanh(y[:, 65])}
+
+    toy = Toy().to(DEV)
+    opt = torch.optim.SGD(toy.parameters(), lr=0.1, momentum=0.9)
+    means = train_epoch(toy, opt, buf.features[:buf.size], buf.policies[:buf.size], buf.values[:buf.size],
+                        batch_size=64)
+    assert all(np.isfinite(v) for v in means.values()) and means["policy_loss"] > 0
+
+    sd2 = alphazero_state_dict(9, 5, 128, 1, 32)
+
+    class Holder(torch.nn.Module):  # stands in for the trained AlphaZeroNet
+        def state_dict(self, *a, **k):
+            return {k_: torch.from_numpy(np.asarray(v)) for k_, v in sd2.items()}
+
+    refresh_native(net, Holder())
+    fresh = om.NativeNet(sd2, device=0)
+    x = buf.features[:300].contiguous()
+    o1, o2 = net(x), fresh(x)
+    assert torch.equal(o1["policy"], o2["policy"]) and torch.equal(o1["value"], o2["value"])
