@@ -188,6 +188,7 @@ def test_gpu_mcts_known_answers(om, case):
     assert m.visit_counts() == case["visit_counts"]
 
 
+import numerics  # noqa: E402
 import ref_fixtures as RF  # noqa: E402
 
 REF_ULP_FLIPS: dict[str, int] = {}
@@ -214,7 +215,7 @@ def test_gpu_mcts_matches_reference_matrix(om, case):
     stub = _torch_stub(O.equivariant_stub if case["stub"] == "equivariant" else O.uniform_stub)
     flips = RF.replay_case(m, case, lambda mm: mm.search(stub), _om_pos, _om_spd)
     REF_ULP_FLIPS[case["name"]] = flips
-    print(f"[parity] ref-matrix {case['name']}: moves={len(case['actions'])} q_ulp_flips={flips}")
+    numerics.record(f"reference MCTS {case['name']}", f"moves={len(case['actions'])} q_ulp_flips={flips}")
 
 
 @pytest.mark.parametrize("gi", [0, 1])
