@@ -172,6 +172,8 @@ def main() -> None:
     ap.add_argument("--eval-batch", type=int, default=0,
                     help="NN rows per ResNet launch (0 = a whole pipeline group, games*L/2 rows); "
                          "configs[4] uses 2048")
+    ap.add_argument("--pipeline", type=int, default=0, help="pipeline groups (0 = engine default: 2)")
+    ap.add_argument("--nn-chains", type=int, default=1, help="concurrent chains of ResNet launches")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
@@ -206,6 +208,9 @@ def main() -> None:
     L = args.threads * args.batch
     if args.eval_batch:  # rows per ResNet launch; the 2 pipeline groups stay
         b.engine.set_nn_batch(args.eval_batch)
+    if args.pipeline:
+        b.engine.set_pipeline(args.pipeline)
+    b.engine.set_nn_chains(args.nn_chains)
     sims_per_search = L * ((args.sims + L - 1) // L)
 
     def step():

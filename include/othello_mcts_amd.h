@@ -163,6 +163,10 @@ int oamd_engine_set_pipeline(oamd_engine *e, int32_t groups);
  * `rows` rows on its stream (the NN evaluation batch; configs[4] uses 2048).
  * Results do not depend on it. */
 int oamd_engine_set_nn_batch(oamd_engine *e, int32_t rows);
+/* The pipeline groups' ResNet launches form `chains` chains (group k in chain
+ * k % chains, 1..4, default 1): launches of one chain run one after another,
+ * chains run concurrently. Results do not depend on it. */
+int oamd_engine_set_nn_chains(oamd_engine *e, int32_t chains);
 /* Diagnostics: copy the ResNet kernel's per-workgroup time stamps (8 u64 per
  * workgroup, 16 u64 per workgroup: see tools/nn_stamps.py) of the last launch. Only in builds
  * with OAMD_EXTRA_FLAGS=-DOAMD_STAMPS; otherwise OAMD_INVALID_ARGUMENT. */

@@ -163,7 +163,12 @@ struct oamd_engine {
     int n_pipe_streams = 0;
     hipStream_t pipe_stream[kMaxPipeline] = {};
     hipEvent_t fork_ev = nullptr;
-    hipEvent_t nn_token = nullptr;
+    // NN tokens: the pipeline groups' ResNet launches form nn_chains chains
+    // (group k in chain k % nn_chains); launches of one chain run one after
+    // another, chains run concurrently (1 = every launch serialised)
+    static constexpr int kMaxChains = 4;
+    hipEvent_t nn_token[kMaxChains] = {};
+    int nn_chains = 1;
     hipStream_t nn_stream = nullptr;
     hipEvent_t sel_ev[kMaxPipeline] = {};
     hipEvent_t nn_ev[kMaxPipeline] = {};
@@ -218,7 +223,8 @@ struct oamd_engine {
     int ensure_streams(int K) {
         if (K <= 1) return OAMD_OK;
         if (!fork_ev) HIPCHK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
-        if (!nn_token) HIPCHK(hipEventCreateWithFlags(&nn_token, hipEventDisableTiming));
+        for (int c = 0; c < kMaxChains; ++c)
+            if (!nn_token[c]) HIPCHK(hipEventCreateWithFlags(&nn_token[c], hipEventDisableTiming));
         if (!nn_stream) HIPCHK(hipStreamCreateWithFlags(&nn_stream, hipStreamNonBlocking));
         while (n_pipe_streams < K) {
             const int k = n_pipe_streams;
@@ -323,7 +329,8 @@ struct oamd_engine {
             (void)hipEventDestroy(nn_ev[k]);
         }
         if (fork_ev) (void)hipEventDestroy(fork_ev);
-        if (nn_token) (void)hipEventDestroy(nn_token);
+        for (int c = 0; c < kMaxChains; ++c)
+            if (nn_token[c]) (void)hipEventDestroy(nn_token[c]);
         if (nn_stream) (void)hipStreamDestroy(nn_stream);
     }
 };
@@ -863,6 +870,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     // rounds 0..steps (k_tree): round s backs up batch s-1 and selects batch s,
     // thread by thread; the NN evaluates batch s between rounds s and s+1
     const int T = e->cfg.num_threads, B = e->cfg.batch_size;
+    const int nch = e->nn_chains < K ? e->nn_chains : K;
     for (int s = 0; s <= steps; ++s) {
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)g0[k] * L;
@@ -877,8 +885,8 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
                 ns = e->nn_stream;
                 HIPCHK(hipEventRecord(e->sel_ev[k], st[k]));
                 HIPCHK(hipStreamWaitEvent(ns, e->sel_ev[k], 0));
-            } else if (K > 1 && OAMD_NN_ORDER == 1 && (s > 0 || k > 0)) {
-                HIPCHK(hipStreamWaitEvent(st[k], e->nn_token, 0));
+            } else if (K > 1 && OAMD_NN_ORDER == 1 && (s > 0 || k >= nch)) {
+                HIPCHK(hipStreamWaitEvent(st[k], e->nn_token[k % nch], 0));
             }
             if (ev) HIPCHK(hipEventRecord(ev[2], ns));
             const int grows = ng[k] * L;
@@ -891,7 +899,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
                 HIPCHK(hipEventRecord(e->nn_ev[k], ns));
                 HIPCHK(hipStreamWaitEvent(st[k], e->nn_ev[k], 0));
             } else if (K > 1 && OAMD_NN_ORDER == 1) {
-                HIPCHK(hipEventRecord(e->nn_token, st[k]));
+                HIPCHK(hipEventRecord(e->nn_token[k % nch], st[k]));
             }
         }
     }
@@ -939,6 +947,13 @@ int oamd_debug_read_stamps(uint64_t* out, int64_t n) {
     const int rc = resnet_read_stamps(reinterpret_cast<unsigned long long*>(out), (long long)n);
     if (rc == -2) return fail(OAMD_INVALID_ARGUMENT, "built without OAMD_STAMPS");
     return rc ? fail(OAMD_RUNTIME, "stamp copy failed") : OAMD_OK;
+}
+
+int oamd_engine_set_nn_chains(oamd_engine* e, int32_t chains) {
+    if (chains < 1 || chains > oamd_engine::kMaxChains)
+        return fail(OAMD_INVALID_ARGUMENT, "nn chains must be in [1, " + std::to_string(oamd_engine::kMaxChains) + "]");
+    e->nn_chains = chains;
+    return OAMD_OK;
 }
 
 int oamd_engine_set_nn_batch(oamd_engine* e, int32_t rows) {
