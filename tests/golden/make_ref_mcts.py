@@ -256,7 +256,43 @@ def make_self_play(om) -> None:
     np.savez_compressed(GOLD / "ref_self_play.npz", **arrays)
 
 
+# ---------------------------------------------------------------- Dirichlet noise statistics
+def make_noise_stats(om) -> None:
+    """The reference's root visit counts under Dirichlet noise (nondeterministic:
+    std::random_device-seeded mt19937, search_thread.cpp:22-24, :233), over
+    many independent runs per setting: a distribution fixture (SURVEY.md §4
+    'Stochastic parts')."""
+    seed, acts, pass_ply = game_with_pass(om)
+    settings = [
+        {"name": "t1_b8_s64_h4_open", "prefix": [], "history_size": 4, "num_threads": 1, "batch_size": 8,
+         "num_simulations": 64, "runs": 400},
+        {"name": "t1_b8_s96_h4_mid", "prefix": acts[:20], "history_size": 4, "num_threads": 1, "batch_size": 8,
+         "num_simulations": 96, "runs": 400},
+        {"name": "t2_b16_s800_h8_open", "prefix": [], "history_size": 8, "num_threads": 2, "batch_size": 16,
+         "num_simulations": 800, "runs": 200},
+    ]
+    arrays = {}
+    for st in settings:
+        rows = []
+        for _ in range(st["runs"]):
+            m = om.MCTS(history_size=st["history_size"], num_simulations=st["num_simulations"],
+                        num_threads=st["num_threads"], batch_size=st["batch_size"], dirichlet_epsilon=0.25,
+                        dirichlet_alpha=0.5)
+            for a in st["prefix"]:
+                m.apply_action(a)
+            m.search(equivariant_stub)
+            rows.append(m.visit_counts())
+        v = np.array(rows, np.int32)
+        arrays[st["name"]] = v
+        print(f"noise {st['name']}: mean {v.mean(0).round(2)} std {v.std(0).round(2)}")
+    (GOLD / "ref_noise.json").write_text(json.dumps({
+        "provenance": "compiled reference, dirichlet_epsilon 0.25, alpha 0.5, equivariant stub; rows = runs",
+        "settings": settings}, indent=0))
+    np.savez_compressed(GOLD / "ref_noise.npz", **arrays)
+
+
 if __name__ == "__main__":
     om = load_ref()
     make_matrix(om)
     make_self_play(om)
+    make_noise_stats(om)

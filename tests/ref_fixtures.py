@@ -98,3 +98,21 @@ def value_targets(num_moves: int, final_p1: int, final_p2: int) -> np.ndarray:
         out += [v] * 8
         v = -v
     return np.array(out, np.float32)
+
+
+def load_noise() -> tuple[list[dict], dict]:
+    meta = json.loads((GOLD / "ref_noise.json").read_text())
+    return meta["settings"], dict(np.load(GOLD / "ref_noise.npz"))
+
+
+def compare_visit_distributions(ours: np.ndarray, ref: np.ndarray) -> tuple[float, float]:
+    """Two-sample comparison of root visit counts (rows = independent runs,
+    columns = root children): the smallest per-child KS p-value times the
+    number of children (Bonferroni), and the largest std ratio deviation."""
+    from scipy import stats
+
+    assert ours.shape[1] == ref.shape[1]
+    k = ours.shape[1]
+    p = min(stats.ks_2samp(ours[:, j], ref[:, j]).pvalue for j in range(k)) * k
+    ratio = max(abs(np.log(ours[:, j].std() / ref[:, j].std())) for j in range(k))
+    return min(p, 1.0), float(np.exp(ratio))

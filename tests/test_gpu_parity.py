@@ -427,3 +427,38 @@ def test_gpu_async_search_matches_sync(om):
     a_async, v_async = play(False)
     np.testing.assert_array_equal(a_sync, a_async)
     assert v_sync == v_async
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2])
+def test_gpu_dirichlet_noise_distribution_matches_reference(om, idx):
+    """The HIP search's root visit counts under Dirichlet noise over independent
+    games vs the compiled reference's over as many runs (tests/golden/ref_noise.*):
+    per-child two-sample KS (Bonferroni p > 1e-3), per-child std within 25 %.
+    Setting 2 is the self-play configuration's thread structure (T=2 x B=16,
+    800 sims, H=8)."""
+    settings, arr = RF.load_noise()
+    st = settings[idx]
+    G = st["runs"]
+    b = om.BatchedMCTS(G, history_size=st["history_size"], num_simulations=st["num_simulations"],
+                       num_threads=st["num_threads"], batch_size=st["batch_size"], dirichlet_epsilon=0.25,
+                       dirichlet_alpha=0.5, seed=91 + idx, node_capacity=1 << 15)
+    for a in st["prefix"]:
+        b.apply_actions(torch.full((G,), a, dtype=torch.int32, device=DEV))
+
+    def stub(features):
+        p, v = O.equivariant_stub(features.cpu().numpy())
+        return {"policy": torch.from_numpy(p), "value": torch.from_numpy(v)}
+
+    b.search(stub)
+    v, _ = b.root_stats()
+    ours = v[:, _legal_of(b)].cpu().numpy()
+    p, r = RF.compare_visit_distributions(ours, arr[st["name"]])
+    numerics.record(f"dirichlet noise {st['name']}", f"games={G} ks_bonferroni_p={p:.3g} max_std_ratio={r:.3f}")
+    assert p > 1e-3 and r < 1.25, (st["name"], p, r)
+
+
+def _legal_of(b):
+    """Root children's actions of game 0 (legal_actions order)."""
+    info = b.root_info(0)
+    legal = info["legal_moves"]
+    return [a for a in range(64) if (legal >> (63 - a)) & 1] or [64]

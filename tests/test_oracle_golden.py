@@ -246,3 +246,26 @@ def test_oracle_reproduces_reference_self_play(gi):
     fin = m.position()
     assert fin.player == 0
     np.testing.assert_array_equal(RF.value_targets(len(g["actions"]), fin.p1, fin.p2), v_exp)
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2])
+def test_oracle_dirichlet_noise_distribution_matches_reference(idx):
+    """SURVEY §4 'Stochastic parts': the reference's root visit counts under
+    Dirichlet noise (eps 0.25, alpha 0.5; its mt19937 is seeded from
+    random_device, so it is pinned by distribution) vs the oracle's over as
+    many independent game keys: per-child two-sample KS (Bonferroni p > 1e-3)
+    and per-child std within 25 %."""
+    settings, arr = RF.load_noise()
+    st = settings[idx]
+    ref = arr[st["name"]]
+    rows = []
+    for key in range(st["runs"]):
+        m = O.OracleMCTS(history_size=st["history_size"], num_simulations=st["num_simulations"],
+                         num_threads=st["num_threads"], batch_size=st["batch_size"], dirichlet_epsilon=0.25,
+                         dirichlet_alpha=0.5, game_key=1000003 * key + 17)
+        for a in st["prefix"]:
+            m.apply_action(a)
+        m.search(O.equivariant_stub)
+        rows.append(m.visit_counts())
+    p, r = RF.compare_visit_distributions(np.array(rows), ref)
+    assert p > 1e-3 and r < 1.25, (st["name"], p, r)
