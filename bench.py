@@ -222,7 +222,7 @@ def main() -> None:
     torch.cuda.synchronize()
     b.engine.enable_timing(max(1, args.timing_every))
     ms0, launches0, rows0 = b.engine.nn_timing()
-    sel0, bk0, _ = b.engine.tree_timing()
+    sel0, bk0, tree_launches0 = b.engine.tree_timing()
 
     def run():
         for _ in range(args.steps):
@@ -230,7 +230,7 @@ def main() -> None:
 
     dt_max = timed_max(world, run, torch.cuda.synchronize, "cpu" if backend == "gloo" else "cuda")
     ms1, launches1, rows1 = b.engine.nn_timing()
-    sel1, bk1, _ = b.engine.tree_timing()
+    sel1, bk1, tree_launches1 = b.engine.tree_timing()
     value = aggregate_rate(world, args.games, sims_per_search, args.steps, dt_max)
     # every game's search followed the reference: no node pool ran out
     overflow_games, depth_capped = b.engine.status()
@@ -281,8 +281,11 @@ def main() -> None:
     # k_tree: one launch per search round and pipeline group; "select" rounds
     # back up the previous batch and select the next, the final round backs up
     tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch)}
-    for name, ms in (("k_tree", sel1 - sel0), ("k_tree_final_backup", bk1 - bk0)):
-        avg = ms / max(1, nn_launches)
+    tree_launches = tree_launches1 - tree_launches0  # select rounds x pipeline groups
+    steps_per_search = (args.sims + L - 1) // L
+    for name, ms, n in (("k_tree", sel1 - sel0, tree_launches),
+                        ("k_tree_final_backup", bk1 - bk0, tree_launches // steps_per_search)):
+        avg = ms / max(1, n)
         entry = {"avg_launch_ms": round(avg, 4)}
         if name in tree_bytes:
             gbs = tree_bytes[name] / (avg * 1e-3) / 1e9

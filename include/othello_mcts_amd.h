@@ -254,13 +254,17 @@ int oamd_engine_game_key(oamd_engine *e, int32_t game, uint64_t *key_host);
 
 /* Timing accumulated over the timed oamd_engine_search calls (HIP events on
  * the launching streams; a query waits for the searches still in flight):
- * total ms spent in the NN kernel, number of NN launches, rows evaluated. */
+ * total ms spent in the NN kernel, number of NN launches, rows evaluated.
+ * With two pipeline groups on prioritised streams (opt-in, OAMD_NN_PRIO=1)
+ * only group 0's launches are counted: group 1's launch is enqueued before it
+ * can dispatch, so its events would include the wait behind group 0's. */
 int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches, int64_t *rows);
 /* Same for the tree kernel (k_tree, one launch per search round and pipeline
  * group): select_ms = total ms of the rounds that select (each also backs up
  * the previous batch, thread by thread), backup_ms = total ms of the final
- * backup-only rounds. launches = NN launches. Timed searches record 4 HIP
- * events per round and pipeline group on the group's stream. */
+ * backup-only rounds (one per search and pipeline group). launches = timed
+ * select rounds (k_tree launches: rounds x pipeline groups). Timed searches
+ * record 4 HIP events per round and pipeline group on the group's stream. */
 int oamd_engine_tree_timing(const oamd_engine *e, float *select_ms, float *backup_ms, int64_t *launches);
 /* enable: 0 off, 1 time every search, N >= 2 time every N-th search (sampled:
  * a timed search's event packets lengthen the gaps between its launches). */

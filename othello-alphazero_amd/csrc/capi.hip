@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -182,6 +183,8 @@ struct oamd_engine {
     std::vector<hipEvent_t> ev[2];
     int ev_blocks[2] = {0, 0};  // pending (round, group) blocks per pool
     int ev_final[2] = {0, 0};   // first block of the backup-only final round
+    int ev_K[2] = {1, 1};       // groups per round of those blocks
+    int ev_nn_groups[2] = {1, 1};  // groups (0 .. n-1) whose NN launches carry events
     int64_t ev_launches[2] = {0, 0};  // k_resnet launches inside those blocks
     int64_t ev_rows[2] = {0, 0};
     int ev_cur = 0;
@@ -189,6 +192,7 @@ struct oamd_engine {
     float select_ms = 0.0f;
     float backup_ms = 0.0f;
     int64_t nn_launches = 0;
+    int64_t tree_launches = 0;  // timed select rounds (one k_tree launch per round and group)
     int64_t nn_rows = 0;
 
     int resolve_timing(int p) {
@@ -199,16 +203,18 @@ struct oamd_engine {
             float ms = 0.0f;
             // blocks of different groups end on different streams; the final
             // round records no NN events
+            const bool nn = i < ev_final[p] && i % ev_K[p] < ev_nn_groups[p];
             HIPCHK(hipEventSynchronize(b[1]));
-            if (i < ev_final[p]) HIPCHK(hipEventSynchronize(b[3]));
+            if (nn) HIPCHK(hipEventSynchronize(b[3]));
             HIPCHK(hipEventElapsedTime(&ms, b[0], b[1]));
             (i < ev_final[p] ? select_ms : backup_ms) += ms;
-            if (i < ev_final[p]) {
+            if (nn) {
                 HIPCHK(hipEventElapsedTime(&ms, b[2], b[3]));
                 nn_ms += ms;
             }
         }
         nn_launches += ev_launches[p];
+        tree_launches += ev_final[p];
         nn_rows += ev_rows[p];
         ev_blocks[p] = 0;
         return OAMD_OK;
@@ -219,6 +225,22 @@ struct oamd_engine {
     }
 
     int L() const { return cfg.num_threads * cfg.batch_size; }
+    // Opt-in (OAMD_NN_PRIO=1 in the environment): two pipeline groups on
+    // prioritised streams (group 0 high, group 1 low); group 1's ResNet launch
+    // no longer waits for group 0's to complete, group 0 still waits for group
+    // 1's previous launch (two priority levels cannot order a cycle). Bench C2,
+    // same box: 4.31 vs 4.27 M sims/s (tools/prio_ab.sh), but the priority does
+    // not hold the dispatch order: the two groups' launches share the CUs for
+    // most of their run (kernel trace: 1.16 / 1.54 ms per launch instead of
+    // 0.91), so a launch's duration no longer measures the kernel. Off by
+    // default, so the bench's roofline stays a per-launch measurement.
+    static bool nn_prio() {
+        static const bool v = [] {
+            const char* e = getenv("OAMD_NN_PRIO");
+            return e ? atoi(e) != 0 : false;
+        }();
+        return v;
+    }
 
     int ensure_streams(int K) {
         if (K <= 1) return OAMD_OK;
@@ -228,7 +250,13 @@ struct oamd_engine {
         if (!nn_stream) HIPCHK(hipStreamCreateWithFlags(&nn_stream, hipStreamNonBlocking));
         while (n_pipe_streams < K) {
             const int k = n_pipe_streams;
-            HIPCHK(hipStreamCreateWithFlags(&pipe_stream[k], hipStreamNonBlocking));
+            if (nn_prio() && K == 2) {
+                int least = 0, greatest = 0;
+                HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+                HIPCHK(hipStreamCreateWithPriority(&pipe_stream[k], hipStreamNonBlocking, k == 0 ? greatest : least));
+            } else {
+                HIPCHK(hipStreamCreateWithFlags(&pipe_stream[k], hipStreamNonBlocking));
+            }
             HIPCHK(hipEventCreateWithFlags(&join_ev[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&sel_ev[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&nn_ev[k], hipEventDisableTiming));
@@ -819,7 +847,7 @@ int oamd_engine_tree_timing(const oamd_engine* ce, float* select_ms, float* back
     if (int rc = e->resolve_all_timing()) return rc;
     if (select_ms) *select_ms = e->select_ms;
     if (backup_ms) *backup_ms = e->backup_ms;
-    if (launches) *launches = e->nn_launches;
+    if (launches) *launches = e->tree_launches;
     return OAMD_OK;
 }
 
@@ -871,6 +899,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     // thread by thread; the NN evaluates batch s between rounds s and s+1
     const int T = e->cfg.num_threads, B = e->cfg.batch_size;
     const int nch = e->nn_chains < K ? e->nn_chains : K;
+    const bool prio = K == 2 && e->nn_prio() && OAMD_NN_ORDER == 1;
     for (int s = 0; s <= steps; ++s) {
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)g0[k] * L;
@@ -885,19 +914,26 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
                 ns = e->nn_stream;
                 HIPCHK(hipEventRecord(e->sel_ev[k], st[k]));
                 HIPCHK(hipStreamWaitEvent(ns, e->sel_ev[k], 0));
+            } else if (prio) {
+                if (k == 0 && s > 0) HIPCHK(hipStreamWaitEvent(st[k], e->nn_token[0], 0));
             } else if (K > 1 && OAMD_NN_ORDER == 1 && (s > 0 || k >= nch)) {
                 HIPCHK(hipStreamWaitEvent(st[k], e->nn_token[k % nch], 0));
             }
-            if (ev) HIPCHK(hipEventRecord(ev[2], ns));
+            // prioritised groups: group 1's launch waits for dispatch behind group 0's,
+            // so only group 0's events bracket a kernel's own run time
+            const bool nn_timed = ev && !(prio && k > 0);
+            if (nn_timed) HIPCHK(hipEventRecord(ev[2], ns));
             const int grows = ng[k] * L;
             const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
             for (int r = 0; r < grows; r += cb)
                 launch_resnet_packed(N, E.feat + (r0 + r) * E.FW, E.FW, E.H, std::min(cb, grows - r),
                                      E.policy + (r0 + r) * 65, E.value + r0 + r, ns);
-            if (ev) HIPCHK(hipEventRecord(ev[3], ns));
+            if (nn_timed) HIPCHK(hipEventRecord(ev[3], ns));
             if (K > 1 && OAMD_NN_ORDER == 2) {
                 HIPCHK(hipEventRecord(e->nn_ev[k], ns));
                 HIPCHK(hipStreamWaitEvent(st[k], e->nn_ev[k], 0));
+            } else if (prio) {
+                if (k == 1) HIPCHK(hipEventRecord(e->nn_token[0], st[k]));
             } else if (K > 1 && OAMD_NN_ORDER == 1) {
                 HIPCHK(hipEventRecord(e->nn_token[k % nch], st[k]));
             }
@@ -913,13 +949,16 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     if (timed) {
         e->ev_blocks[pool] = (steps + 1) * K;
         e->ev_final[pool] = steps * K;
-        int64_t nl = 0;
-        for (int k = 0; k < K; ++k) {
+        e->ev_K[pool] = K;
+        e->ev_nn_groups[pool] = prio ? 1 : K;
+        int64_t nl = 0, rows = 0;
+        for (int k = 0; k < e->ev_nn_groups[pool]; ++k) {
             const int grows = ng[k] * L, cb = e->nn_batch > 0 ? e->nn_batch : grows;
             nl += (grows + cb - 1) / cb;
+            rows += grows;
         }
         e->ev_launches[pool] = (int64_t)steps * nl;
-        e->ev_rows[pool] = (int64_t)steps * e->G * L;
+        e->ev_rows[pool] = (int64_t)steps * rows;
         e->ev_cur ^= 1;
     }
     // without counters requested the search is left in flight (stream order)
