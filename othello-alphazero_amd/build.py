@@ -35,8 +35,11 @@ UNITS = {
     "tree.hip": EXACT,
     "capi.hip": EXACT,
     # accumulators and fragments in arch VGPRs: the default heuristic parks the
-    # 128 accumulators of a 1-wave/SIMD tile in AGPRs and shuffles them per MFMA
-    "resnet.hip": os.environ.get("OAMD_RESNET_FLAGS", "-mllvm -amdgpu-mfma-vgpr-form=1").split()
+    # 128 accumulators of a 1-wave/SIMD tile in AGPRs and shuffles them per MFMA;
+    # the max-ILP machine scheduler: k_resnet_w8 0.895-0.900 vs 0.907-0.913 ms per
+    # 4096 rows (3 same-box pairs, outputs bit-identical; tools/ab_run1.sh)
+    "resnet.hip": os.environ.get("OAMD_RESNET_FLAGS",
+                                 "-mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp").split()
     + ["-Rpass-analysis=kernel-resource-usage"],
 }
 
