@@ -152,7 +152,10 @@ int oamd_engine_reset(oamd_engine *e, int32_t game, uint64_t seed);
  * (MCTS::search, mcts.h:220-256). Outputs are optional (may be NULL):
  * simulations = leaf selections (sum over games), evaluations = NN rows of
  * non-terminal leaves. With both NULL the call returns once the search is
- * enqueued (stream order; the host does not wait), otherwise after it ends. */
+ * enqueued (stream order; the host does not wait), otherwise after it ends.
+ * One game with num_threads > 1 runs thread by thread, each thread's ResNet
+ * rows on a stream of their own while the next thread's tree work runs
+ * (same results; OAMD_TREE_SPLIT=0 in the environment turns it off). */
 int oamd_engine_search(oamd_engine *e, oamd_net *net, int64_t *simulations, int64_t *evaluations);
 /* Split the games into `groups` pipeline groups (own HIP streams) so that tree
  * kernels of one group overlap the NN launch of another (0 = auto: 2 groups

@@ -234,6 +234,14 @@ struct oamd_engine {
     // most of their run (kernel trace: 1.16 / 1.54 ms per launch instead of
     // 0.91), so a launch's duration no longer measures the kernel. Off by
     // default, so the bench's roofline stays a per-launch measurement.
+    // thread-split schedule for one game (OAMD_TREE_SPLIT=0 in the environment: off)
+    static bool tree_split() {
+        static const bool v = [] {
+            const char* e = getenv("OAMD_TREE_SPLIT");
+            return e ? atoi(e) != 0 : true;
+        }();
+        return v;
+    }
     static bool nn_prio() {
         static const bool v = [] {
             const char* e = getenv("OAMD_NN_PRIO");
@@ -868,7 +876,17 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     int K = e->pipeline > 0 ? e->pipeline : (e->G >= 64 ? 2 : 1);
     if (K > e->G) K = e->G;
     if (K > kMaxPipeline) K = kMaxPipeline;
-    int rc = e->ensure_streams(K);
+    const int T = e->cfg.num_threads, B = e->cfg.batch_size;
+    // One game with T > 1 virtual threads (the drop-in MCTS, latency mode):
+    // the tree kernel runs thread by thread on the engine stream, and thread
+    // t's ResNet rows go to a stream of their own as soon as its selection is
+    // done, so they are evaluated while the tree kernel backs up and selects
+    // for thread t+1 (the overlap the reference gets from its T threads,
+    // search_thread.cpp:59-128). The order of the tree operations is the same
+    // as in one launch per round, so results are identical.
+    const bool split = e->G == 1 && K == 1 && T > 1 && T <= kMaxPipeline && e->tree_split();
+    const int NB = split ? T : K;  // timing blocks per round
+    int rc = e->ensure_streams(split ? T : K);
     if (rc) return rc;
     if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
     // sampled timing: every timing_stride-th search records its events
@@ -878,7 +896,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     const int pool = e->ev_cur;
     if (timed) {
         if ((rc = e->resolve_timing(pool))) return rc;
-        while ((int)e->ev[pool].size() < kEvPerBlock * (steps + 1) * K) {
+        while ((int)e->ev[pool].size() < kEvPerBlock * (steps + 1) * NB) {
             hipEvent_t x;
             HIPCHK(hipEventCreate(&x));
             e->ev[pool].push_back(x);
@@ -897,10 +915,27 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     }
     // rounds 0..steps (k_tree): round s backs up batch s-1 and selects batch s,
     // thread by thread; the NN evaluates batch s between rounds s and s+1
-    const int T = e->cfg.num_threads, B = e->cfg.batch_size;
     const int nch = e->nn_chains < K ? e->nn_chains : K;
     const bool prio = K == 2 && e->nn_prio() && OAMD_NN_ORDER == 1;
-    for (int s = 0; s <= steps; ++s) {
+    for (int s = 0; split && s <= steps; ++s) {
+        for (int t = 0; t < T; ++t) {
+            hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * T + t)] : nullptr;
+            if (s > 0) HIPCHK(hipStreamWaitEvent(e->stream, e->nn_ev[t], 0));  // thread t's batch s-1 evaluated
+            if (ev) HIPCHK(hipEventRecord(ev[0], e->stream));
+            launch_tree(E, e->stream, s > 0, s < steps, T, B, 0, 1, t, t + 1);
+            if (ev) HIPCHK(hipEventRecord(ev[1], e->stream));
+            if (s == steps) continue;
+            hipStream_t ns = e->pipe_stream[t % 2];
+            HIPCHK(hipEventRecord(e->sel_ev[t], e->stream));
+            HIPCHK(hipStreamWaitEvent(ns, e->sel_ev[t], 0));
+            if (ev) HIPCHK(hipEventRecord(ev[2], ns));
+            launch_resnet_packed(N, E.feat + (size_t)t * B * E.FW, E.FW, E.H, B, E.policy + (size_t)t * B * 65,
+                                 E.value + (size_t)t * B, ns);
+            if (ev) HIPCHK(hipEventRecord(ev[3], ns));
+            HIPCHK(hipEventRecord(e->nn_ev[t], ns));
+        }
+    }
+    for (int s = 0; !split && s <= steps; ++s) {
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)g0[k] * L;
             hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
@@ -947,12 +982,16 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
         }
     }
     if (timed) {
-        e->ev_blocks[pool] = (steps + 1) * K;
-        e->ev_final[pool] = steps * K;
-        e->ev_K[pool] = K;
-        e->ev_nn_groups[pool] = prio ? 1 : K;
+        e->ev_blocks[pool] = (steps + 1) * NB;
+        e->ev_final[pool] = steps * NB;
+        e->ev_K[pool] = NB;
+        e->ev_nn_groups[pool] = prio ? 1 : NB;
         int64_t nl = 0, rows = 0;
-        for (int k = 0; k < e->ev_nn_groups[pool]; ++k) {
+        if (split) {
+            nl = T;
+            rows = L;
+        }
+        for (int k = 0; !split && k < e->ev_nn_groups[pool]; ++k) {
             const int grows = ng[k] * L, cb = e->nn_batch > 0 ? e->nn_batch : grows;
             nl += (grows + cb - 1) / cb;
             rows += grows;

@@ -19,10 +19,11 @@ struct SelfplayParams {
 
 // tree.hip
 // One search round for games [g0, g0 + ng) (ng < 0: to the end): for each
-// virtual thread t < T, back up its previous batch (do_backup), then select its
-// next B leaves (do_select). T * B must equal E.L. See tree.hip k_tree.
+// virtual thread t in [t0, t1) (t1 < 0: T), back up its previous batch
+// (do_backup), then select its next B leaves (do_select). T * B must equal
+// E.L. See tree.hip k_tree.
 void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
-                 int g0 = 0, int ng = -1);
+                 int g0 = 0, int ng = -1, int t0 = 0, int t1 = -1);
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s);
 void launch_set_evaluation(const EngineView& E, const float* pol, const float* val, int row_begin,
                            int rows, hipStream_t s);

@@ -446,7 +446,7 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
 // runs on the CUs that the other group's ResNet launch occupies. The cap costs
 // two 8-byte spills outside the descent/backup loops.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree(EngineView E, int g0, int do_backup, int do_select,
-                                             int T, int B) {
+                                             int t0, int t1, int B) {
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     GameState* gs = E.games + g;
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     const int flags = gs->flags;
     if (!(flags & kActive)) {
         if (do_select) {
-            for (int i = 0; i < E.L; ++i) {
+            for (int i = t0 * B; i < t1 * B; ++i) {
                 const int r = g * E.L + i;
                 if (lane == 0) {
                     E.leaf[r] = -1;
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     unsigned long long sims = 0, evals = 0;
     int count = gs->count;
     bool overflow = false;
-    for (int t = 0; t < T; ++t) {
+    for (int t = t0; t < t1; ++t) {
         if (do_backup) backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
         if (do_select) select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals);
     }
@@ -877,11 +877,12 @@ __global__ void k_apply_positions(const Pos* in, const int32_t* actions, Pos* ou
 static inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
-                 int g0, int ng) {
+                 int g0, int ng, int t0, int t1) {
     if (ng < 0) ng = E.G - g0;
-    if (T * B != E.L) return;  // caller validated; never launch on a mismatched layout
+    if (t1 < 0) t1 = T;
+    if (T * B != E.L || t0 < 0 || t1 > T || t0 >= t1) return;  // caller validated; never launch on a mismatched layout
     if (ng > 0 && (do_backup || do_select))
-        hipLaunchKernelGGL(k_tree, dim3(ng), dim3(64), 0, s, E, g0, (int)do_backup, (int)do_select, T, B);
+        hipLaunchKernelGGL(k_tree, dim3(ng), dim3(64), 0, s, E, g0, (int)do_backup, (int)do_select, t0, t1, B);
 }
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s) {
     if (rows > 0) hipLaunchKernelGGL(k_features_f32, dim3(blocks_for(rows, 4)), dim3(256), 0, s, E, out, row_begin, rows);

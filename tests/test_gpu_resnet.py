@@ -125,6 +125,32 @@ def test_native_search_equals_callback_search(om):
         assert torch.equal(xa, xb)
 
 
+@pytest.mark.parametrize("threads,batch", [(2, 16), (3, 8), (4, 4)])
+def test_single_game_thread_split_equals_callback_search(om, threads, batch):
+    """One game with T > 1 runs the thread-split schedule (thread t's ResNet rows
+    on their own stream while the tree kernel serves thread t+1); the callback
+    path backs up and selects in the same order through the step API. Visits,
+    Q and the move choices must agree exactly, with Dirichlet noise and tree
+    reuse."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(11, 9, 128, 2, 32), device=0)
+    kw = dict(history_size=4, num_simulations=200, num_threads=threads, batch_size=batch,
+              dirichlet_epsilon=0.25, seed=33, node_capacity=1 << 16)
+    a = om.BatchedMCTS(1, **kw)
+    b = om.BatchedMCTS(1, **kw)
+    a.random_openings(6, seed=2)
+    b.random_openings(6, seed=2)
+    for _ in range(4):
+        a.search(net)
+        b.search(lambda f: net(f))
+        assert a.visit_counts(0) == b.visit_counts(0)
+        assert a.mean_action_values(0) == b.mean_action_values(0)
+        xa = a.selfplay_move(temperature_moves=12)["actions"].cpu()
+        xb = b.selfplay_move(temperature_moves=12)["actions"].cpu()
+        assert torch.equal(xa, xb)
+
+
 def test_mcts_autodetects_alphazero_module(om):
     """MCTS.search(AlphaZeroNet-shaped module) runs the native path, refreshes
     after in-place weight updates, and agrees with NativeNet."""

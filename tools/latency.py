@@ -44,14 +44,17 @@ def run(net, sims, eps, moves):
 
 
 def breakdown(net, sims, moves, eps=0.25):
-    """Per-step kernel time of the same single-game search (HIP events)."""
+    """Kernel time per move of the same single-game search (HIP events): tree
+    kernel launches and ResNet launches (with T > 1 threads one game runs them
+    thread by thread, a thread's ResNet rows overlapping the next thread's tree
+    work, so tree + NN can exceed the wall time)."""
     b = om.BatchedMCTS(1, history_size=8, num_simulations=sims, num_threads=2, batch_size=16, seed=5,
                        dirichlet_epsilon=eps)
     b.search(net)
     b.selfplay_move(temperature_moves=0)
     b.engine.enable_timing(True)
     nn0, l0, _ = b.engine.nn_timing()
-    s0, k0, _ = b.engine.tree_timing()
+    s0, k0, t0_ = b.engine.tree_timing()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(moves):
@@ -60,11 +63,13 @@ def breakdown(net, sims, moves, eps=0.25):
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) * 1e3
     nn1, l1, _ = b.engine.nn_timing()
-    s1, k1, _ = b.engine.tree_timing()
-    n = max(1, l1 - l0)
-    return {"setting": f"BatchedMCTS(1), {sims} sims, eps={eps}", "steps": n, "wall_ms_per_move": round(wall / moves, 2),
-            "select_us_per_step": round((s1 - s0) / n * 1e3, 1), "nn_us_per_step": round((nn1 - nn0) / n * 1e3, 1),
-            "backup_us_per_step": round((k1 - k0) / n * 1e3, 1)}
+    s1, k1, t1_ = b.engine.tree_timing()
+    return {"setting": f"BatchedMCTS(1), {sims} sims, eps={eps}", "moves": moves,
+            "wall_ms_per_move": round(wall / moves, 2),
+            "tree_launches_per_move": (t1_ - t0_) / moves, "nn_launches_per_move": (l1 - l0) / moves,
+            "tree_ms_per_move": round((s1 - s0 + k1 - k0) / moves, 2), "nn_ms_per_move": round((nn1 - nn0) / moves, 2),
+            "tree_us_per_launch": round((s1 - s0) / max(1, t1_ - t0_) * 1e3, 1),
+            "nn_us_per_launch": round((nn1 - nn0) / max(1, l1 - l0) * 1e3, 1)}
 
 
 def main():
