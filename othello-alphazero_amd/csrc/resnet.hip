@@ -284,8 +284,15 @@ using Geo = GeoT<C, 512 / C, C == 256 ? OAMD_WC256 : OAMD_WC, OAMD_REGSTAGE ? 2 
 #ifndef OAMD_SMALL_RING
 #define OAMD_SMALL_RING 4
 #endif
+// waves per board in the small-batch geometry: 8 (16 channels each at C=128)
+// take 0.098 ms per 16-32 rows against 0.107 with 4 (tools/small_ab.sh, two
+// same-box pairs, bit-identical): in this latency regime the per-K-step chain
+// of one wave, not the fragment reads per MFMA, sets the time
+#ifndef OAMD_SMALL_WC_DIV
+#define OAMD_SMALL_WC_DIV 8
+#endif
 template <int C>
-using GeoS = GeoT<C, 1, C / 4, OAMD_REGSTAGE ? 2 : OAMD_SMALL_RING>;
+using GeoS = GeoT<C, 1, C / OAMD_SMALL_WC_DIV, OAMD_REGSTAGE ? 2 : OAMD_SMALL_RING>;
 // two workgroups per CU (C=128): 2 boards and 8 KiB stages per workgroup
 // (79 KB of LDS), so one workgroup's barriers and epilogues can overlap the
 // other's MFMAs, at twice the weight streaming per FLOP
