@@ -150,6 +150,9 @@ static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the 
 #ifndef OAMD_STAGGER
 #define OAMD_STAGGER 0
 #endif
+#ifndef OAMD_PRIO_ALL
+#define OAMD_PRIO_ALL 1  // s_setprio of every ResNet wave, throughput geometry (0 = off)
+#endif
 template <int C>
 __host__ __device__ constexpr int stage_bytes() { return C == 128 ? OAMD_STAGE128 : 16384; }
 
@@ -849,6 +852,12 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     OAMD_STAMP(1);
     if constexpr (OAMD_PRIO_STATIC && G::WAVES == 8)
         if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    // throughput geometry: every ResNet wave issues ahead of the other pipeline
+    // group's co-resident tree waves (SQ arbitration): bench C2 4.42-4.47 vs
+    // 4.31-4.36 M sims/s (tools/bench_ab.sh, four same-box pairs on two boxes),
+    // launch 0.90-0.91 vs 0.92-0.935 ms (the standalone speed), the tree round
+    // 0.46 vs 0.34 ms and still hidden behind the other group's launch
+    if constexpr (OAMD_PRIO_ALL > 0 && G::BOARDS > 1) __builtin_amdgcn_s_setprio(OAMD_PRIO_ALL);
 
     const int nlayers = 1 + 2 * N.R;
     // one conv layer: KIND 0 = first conv, 1 = a block's first conv (saves the
