@@ -9,7 +9,7 @@ i=0
 for f in "${SETS[@]}"; do
   i=$((i+1))
   OAMD_EXTRA_FLAGS="$f" python othello-alphazero_amd/build.py --force > gpurun_out/bab_build.log 2>&1 || { tail gpurun_out/bab_build.log; exit 1; }
-  timeout -k 10 200 python bench.py --cpu-baseline-seconds 0 --steps ${STEPS:-10} > gpurun_out/bab_$i.log 2>&1 || { tail -5 gpurun_out/bab_$i.log; exit 1; }
+  timeout -k 10 300 python bench.py --cpu-baseline-seconds 0 --steps ${STEPS:-10} ${BENCH_EXTRA:-} > gpurun_out/bab_$i.log 2>&1 || { tail -5 gpurun_out/bab_$i.log; exit 1; }
   python3 - "$i" "$f" <<'PY'
 import json, sys
 d = json.loads(open(f"gpurun_out/bab_{sys.argv[1]}.log").read().strip().splitlines()[-1])
