@@ -55,10 +55,13 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 #ifndef OAMD_WC
 #define OAMD_WC 64
 #endif
-// C=256 (2 boards per workgroup, one K-step per 16 KiB stage): 128-channel wave
-// tiles halve the barriers per MFMA and measure 7.8 % faster than 64 (same box)
+// C=256 (2 boards per workgroup, one K-step per 16 KiB stage): 64-channel wave
+// tiles (8 waves, 2 per SIMD) take 7.56 ms per 4096 rows of 256x20b against
+// 8.19-8.21 with 128-channel tiles (4 waves) under the max-ILP scheduler
+// (round 2, two same-box pairs, bit-identical; round 1's default scheduler
+// had ranked them the other way, 7.8 %)
 #ifndef OAMD_WC256
-#define OAMD_WC256 128
+#define OAMD_WC256 64
 #endif
 constexpr int kLdsBytes = 160 * 1024;
 constexpr int kMaxStampWgs = 1 << 16;
