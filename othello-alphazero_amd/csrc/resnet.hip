@@ -153,6 +153,25 @@ static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the 
 #ifndef OAMD_STAGGER
 #define OAMD_STAGGER 0
 #endif
+// Edge-row tiling with zero-tap skipping (throughput geometry, C=128): a
+// 16-position MFMA tile is one board row of two boards, so at the three
+// dy = -1 taps the row-0 tiles (and at dy = +1 the row-7 tiles) read only the
+// zero border and their MFMAs are skipped: 8.3 % of the tower's MFMAs. Waves
+// 0-3 own rows 0-3, their SIMD partners 4-7 rows 7-4. The tower's K order
+// pairs tap a (dy = -1) with tap a + 6 (dy = +1) in one weight stage (same
+// 32-channel block), so every wave skips one of each such stage's two K-steps
+// and the stage barrier stays balanced (kPairOrder; the order is shared by the
+// host packer and every geometry, so all geometries stay bit-identical).
+// The skipped tile's MFMAs are issued last in their K-step, behind a
+// wave-uniform branch (one kernel body). k_resnet_w8, 4096 rows: 0.868-0.872
+// vs 0.887-0.895 ms (two same-box rounds, tools/ab_prebuilt.sh); one body per
+// wave half with compile-time skips measured the same (0.872-0.873, a few
+// spills), and waves 4-7 taking a paired stage's K-steps in swapped order (so
+// every wave skips in the same step) 0.876-0.877: not kept.
+#ifndef OAMD_EDGE
+#define OAMD_EDGE 1
+#endif
+__host__ __device__ constexpr bool kPairOrder(int C) { return OAMD_EDGE != 0 && C == 128; }
 #ifndef OAMD_PRIO_ALL
 #define OAMD_PRIO_ALL 1  // s_setprio of every ResNet wave, throughput geometry (0 = off)
 #endif
@@ -195,9 +214,16 @@ void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad) {
         *tap = i < 9 ? i : 8;
         *cb = 0;
         *pad = i >= 9;
+    } else if (kPairOrder(C) && i < 6 * (C / 32)) {
+        // stage i/2 = (tap a, block cb), (tap a + 6, block cb)
+        const int pi = i / 2;
+        *tap = pi / (C / 32) + (i & 1) * 6;
+        *cb = pi % (C / 32);
+        *pad = false;
     } else {
-        *tap = i / (C / 32);
-        *cb = i % (C / 32);
+        const int j = kPairOrder(C) ? i - 6 * (C / 32) : i;
+        *tap = (kPairOrder(C) ? 3 : 0) + j / (C / 32);
+        *cb = j % (C / 32);
         *pad = false;
     }
 }
@@ -232,6 +258,26 @@ constexpr TilePos make_tile_pos() {
 }
 __constant__ TilePos kTilePos = make_tile_pos();
 
+// Edge-row tiling (G::EDGE): padded row of B-fragment column j of position tile
+// m for position group q (wave / WN). Group q = (pair P, half h): tile m is
+// board row y = h ? 7 - m : m of boards P and P + NPAIR (NPAIR * BROWS = 8 mod
+// 16 rows apart, so the tile's 16 squares cover every residue of the padded row
+// mod 16 once). Columns 0-3 / 12-15 take the odd-residue squares of board P /
+// P + NPAIR, columns 4-7 / 8-11 the even ones: the kTilePos split, so the
+// kgroup_chunk map keeps every ds_read_b128 lane group on 16 distinct slots
+// (tests/test_cpu_host.py restates and checks it for every tap).
+template <class G>
+__host__ __device__ constexpr int edge_tile_row(int q, int m, int j) {
+    constexpr int NP = G::NPAIR > 0 ? G::NPAIR : 1;
+    const int P = q % NP, h = q / NP;
+    const int y = h ? 7 - m : m;
+    const int r0 = (P * G::BROWS + (y + 1) * 10 + 1) & 15;
+    const int oddcol = (j < 4 || j >= 12) ? 1 : 0;
+    const int b = j < 8 ? P : P + NP;
+    const int x = 2 * (j & 3) + ((r0 & 1) ^ oddcol);
+    return b * G::BROWS + (y + 1) * 10 + x + 1;
+}
+
 // Workgroup geometry: C channels, BOARDS boards per workgroup, WC output
 // channels per wave (NT = WC/16 MFMA tiles), at most RING_MAX weight slots of
 // STAGE bytes (a whole number of K-steps; the packed weights are K-step
@@ -246,7 +292,12 @@ struct GeoT {
     static constexpr int WAVES = BOARDS * WN;
     static constexpr int THREADS = WAVES * 64;
     static constexpr int RP = 2 * C + 16;       // row pitch (bytes)
-    static constexpr int BROWS = 100;           // 10x10 padded board
+    // board stride in rows (10x10 padded board); with two boards per workgroup
+    // 104, so the two boards of an edge tile sit 8 rows apart modulo 16
+    static constexpr int BROWS = BOARDS_ == 2 && kPairOrder(C_) ? 104 : 100;
+    static constexpr int NPAIR = BOARDS / 2;
+    static constexpr bool EDGE = kPairOrder(C_) && BOARDS >= 2 && BOARDS % 2 == 0 && !OAMD_STAGGER &&
+                                 STAGE_ == 2 * 32 * C_ * 2;
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
     static constexpr int KSTEP_BYTES = 32 * C * 2;
     static constexpr int STAGE = STAGE_;
@@ -279,6 +330,7 @@ struct GeoT {
     static_assert(RING >= (OAMD_REGSTAGE ? 2 : 3) && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
     static_assert(ksteps_first(C) % KS == 0 && ksteps_tower(C) % KS == 0, "whole stages per layer");
     static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 63, "decomposition");
+    static_assert(!EDGE || ((NPAIR * BROWS) % 16 == 8 && WAVES == 8), "edge tiles: pair boards 8 rows apart mod 16");
 };
 // throughput geometry: 512 positions x C channels per workgroup, 8 waves
 template <int C>
@@ -409,6 +461,12 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 template <int DT, int NT>
+__device__ __forceinline__ void mfma_tile0(f32x4_t (&acc)[NT][4], const Frags<NT>& f) {
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n][0] = mfma<DT>(f.w[n], f.x[0], acc[n][0]);
+}
+
+template <int DT, int NT>
 __device__ __forceinline__ void mfma_half(f32x4_t (&acc)[NT][4], const Frags<NT>& f, int h) {
 #pragma unroll
     for (int n = h * NT / 2; n < (h + 1) * NT / 2; ++n)
@@ -416,13 +474,14 @@ __device__ __forceinline__ void mfma_half(f32x4_t (&acc)[NT][4], const Frags<NT>
         for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
 }
 
-template <int DT, int NT>
+// SK: tile 0's MFMAs are left out (edge tiling: issued separately, mfma_tile0)
+template <int DT, bool SK = false, int NT>
 __device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[NT][4], const Frags<NT>& f) {
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
-        for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
+        for (int m = SK ? 1 : 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -716,7 +775,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
-    const int wm = wave / G::WN;  // board of this wave
+    const int wm = wave / G::WN;  // board of this wave (EDGE: position group, edge_tile_row)
     const int wn = wave % G::WN;  // OAMD_WC-channel block of this wave
     const int kg = lane >> 4;
     const int row0 = blockIdx.x * G::BOARDS;
@@ -768,7 +827,9 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     int rd[4], wr[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-        const int rowb = (wm * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) * G::RP;
+        const int rowb = (G::EDGE ? edge_tile_row<G>(wm, m, lane & 15)
+                                  : wm * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) *
+                         G::RP;
         rd[m] = rowb + kgroup_chunk(kg) * 16;
         wr[m] = rowb + wn * G::WC * 2 + kg * 8;
     }
@@ -870,6 +931,9 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         constexpr int kind = decltype(KIND)::value;
         constexpr bool first = kind == 0;
         constexpr int nk = first ? ksteps_first(C) : ksteps_tower(C);
+        // edge skipping: which wave half (SIMD partners) this wave is in
+        using RtSkip = std::bool_constant<G::EDGE && !first>;
+        const int ehalf = __builtin_amdgcn_readfirstlane(wm / (G::NPAIR > 0 ? G::NPAIR : 1));
 
         // accumulators start at bias (+ block input for the block's second conv)
 #pragma unroll
@@ -893,9 +957,13 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         // of cur's MFMAs go before the barrier, so while waves 0-3 issue the
         // post-barrier DMA and reads, their partners keep the MFMA pipe busy
         // xoff: uniform byte offset of the next K-step's activation rows/channels
-        auto step = [&](auto NEW, auto GB, const Frags<kNT>& cur, Frags<kNT>& nxt, int xoff) {
+        // RTS (edge tiling): cur's tile-0 MFMAs are issued last, behind a
+        // wave-uniform branch on rsk (tile 0 of cur lies on the zero border)
+        auto step = [&](auto NEW, auto GB, const Frags<kNT>& cur, Frags<kNT>& nxt, int xoff, auto RTS, bool rsk) {
+            constexpr bool rts = decltype(RTS)::value;
             constexpr bool open = decltype(NEW)::value;
             constexpr bool gb = decltype(GB)::value;
+            static_assert(!(gb && rts), "stagger without edge skipping");
 #if OAMD_FENCE
             // keep each step's MFMAs (on cur) with the fragment reads they hide:
             // without this fence the scheduler may hoist the next step's MFMAs over
@@ -982,7 +1050,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             if constexpr (gb) {
                 mfma_half<DT>(acc, cur, 1);
             } else {
-                mfma_frags<DT>(acc, cur);
+                mfma_frags<DT, rts>(acc, cur);
             }
 #if OAMD_READS_FIRST
             // issue the 8 fragment reads first, the stage DMA a few MFMAs later
@@ -999,7 +1067,14 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             // fine interleave of the step's fragment reads with its 16 MFMAs: a
             // stage-opening step has the 4 weight reads after the barrier (the
             // activation reads precede it, OAMD_XEARLY), the other step all 8
-            if constexpr (!gb) {
+            if constexpr (!gb && rts) {
+                constexpr int nds = open && OAMD_XEARLY && !G::EARLY ? 4 : 8;
+                static_for<nds>([&](auto I) {
+                    constexpr int i = decltype(I)::value;
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * 12 / nds - i * 12 / nds, 0);
+                });
+            } else if constexpr (!gb) {
                 constexpr int nds = open && OAMD_XEARLY && !G::EARLY ? 4 : 8;
                 if constexpr (OAMD_ILV == 2 && open) __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
                 if constexpr (OAMD_ILV == 5 && open) {  // DMA after the first read + 4 MFMAs
@@ -1029,18 +1104,22 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     __builtin_amdgcn_sched_group_barrier(0x008, kNT * 4 - nds * (OAMD_ILV_SPAN / nds), 0);
             }
 #endif
+            if constexpr (rts) {
+                if (!rsk) mfma_tile0<DT>(acc, cur);
+            }
         };
         using NewOdd = std::integral_constant<bool, G::KS == 1>;  // K-step i1 odd
         using NewEven = std::integral_constant<bool, true>;       // K-step i1 even
+        using NoSkip = std::false_type;
         auto kloop = [&](auto GB) {
             if constexpr (first) {
                 int i = 0;
                 for (; i + 2 < nk; i += 2) {
-                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(i + 1, true));
-                    step(NewEven{}, GB, fb, fa, kstep_offset<C>(i + 2, true));
+                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(i + 1, true), NoSkip{}, false);
+                    step(NewEven{}, GB, fb, fa, kstep_offset<C>(i + 2, true), NoSkip{}, false);
                 }
                 if constexpr (nk % 2 == 0) {
-                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(nk - 1, true));
+                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(nk - 1, true), NoSkip{}, false);
                     mfma_frags<DT>(acc, fb);
                 } else {
                     mfma_frags<DT>(acc, fa);
@@ -1061,17 +1140,45 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                         // the loaded K-step t*KPT + c + 1 opens a stage when it is even
                         using NEW = std::integral_constant<bool, G::KS == 1 || (c + 1) % 2 == 0>;
                         const int xoff = c + 1 == KPT ? tn : to + (c + 1) * 64;
-                        if constexpr (c % 2 == 0) step(NEW{}, GB, fa, fb, xoff);
-                        else step(NEW{}, GB, fb, fa, xoff);
+                        if constexpr (c % 2 == 0) step(NEW{}, GB, fa, fb, xoff, NoSkip{}, false);
+                        else step(NEW{}, GB, fb, fa, xoff, NoSkip{}, false);
                     });
                 };
-                for (int t = 0; t < 8; ++t) tap_steps(t, std::false_type{});
-                tap_steps(8, std::true_type{});
-                mfma_frags<DT>(acc, fb);  // K-step 9*KPT - 1 (odd c)
+                if constexpr (kPairOrder(C)) {
+                    // taps 0-2 paired with 6-8 (stage = (a, cb), (a + 6, cb)), then
+                    // taps 3-5 tap-major. K-step parity <-> fa / fb as before.
+                    static_assert(KPT == 4 && G::KS == 2, "pair order: 2 K-steps per stage");
+                    constexpr int D20 = 20 * G::RP;  // tap a -> a + 6 (dy -1 -> +1)
+                    auto pair_steps = [&](int a, auto LASTA) {
+                        constexpr bool lasta = decltype(LASTA)::value;
+                        const int to = tapoff(a);
+                        const int tn = lasta ? tapoff(3) : to + G::RP;  // tapoff(a + 1), a < 2
+                        static_for<KPT>([&](auto J) {
+                            constexpr int cb = decltype(J)::value;
+                            // cur = (a, cb) in fa: waves 0-3 skip row 0; load (a + 6, cb)
+                            step(std::false_type{}, GB, fa, fb, to + D20 + cb * 64, RtSkip{}, ehalf == 0);
+                            // cur = (a + 6, cb) in fb: waves 4-7 skip row 7; load the next stage
+                            const int xo = cb + 1 < KPT ? to + (cb + 1) * 64 : tn;
+                            step(std::true_type{}, GB, fb, fa, xo, RtSkip{}, ehalf != 0);
+                        });
+                    };
+#pragma nounroll
+                    for (int a = 0; a < 2; ++a) pair_steps(a, std::false_type{});
+                    pair_steps(2, std::true_type{});
+#pragma nounroll
+                    for (int t = 3; t < 5; ++t) tap_steps(t, std::false_type{});
+                    tap_steps(5, std::true_type{});
+                    mfma_frags<DT>(acc, fb);  // K-step 9*KPT - 1 (odd c)
+                } else {
+                    for (int t = 0; t < 8; ++t) tap_steps(t, std::false_type{});
+                    tap_steps(8, std::true_type{});
+                    mfma_frags<DT>(acc, fb);  // K-step 9*KPT - 1 (odd c)
+                }
             }
         };
-        if (OAMD_STAGGER && wave >= 4) {
-            kloop(std::true_type{});
+        if constexpr (OAMD_STAGGER) {
+            if (wave >= 4) kloop(std::true_type{});
+            else kloop(std::false_type{});
         } else {
             kloop(std::false_type{});
         }
@@ -1134,7 +1241,8 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 // of the layer already waited for it
                 if constexpr (!OAMD_REGSTAGE && !G::EARLY) wait_vm<G::VM_LAYER>();
                 lds_barrier();           // ... and this layer's output is complete
-                load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false), rd, wl);
+                load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false),
+                           rd, wl);
             }
 #ifdef OAMD_STAMPS
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -182,17 +182,50 @@ def test_resnet_activation_layout_is_bank_conflict_free():
     def chunk(kg):
         return ((kg & 1) << 1) | (kg >> 1)
 
-    for C in (128, 256):
+    def stride(C):  # GeoT::BROWS: board stride in rows
+        return 104 if 512 // C == 2 else 100
+
+    def conflict_free(C, rows):  # rows[lane & 15] = padded row of the lane's square
         pitch = 2 * C + 16
+        for t in range(9):
+            shift = (t // 3 - 1) * 10 + (t % 3 - 1)
+            for kc in range(C // 32):
+                for g in groups:
+                    addrs = [(rows[lane & 15] + shift) * pitch + (kc * 4 + chunk(lane >> 4)) * 16 for lane in g]
+                    if len({(a // 16) % 16 for a in addrs}) != 16:
+                        return False
+        return True
+
+    for C in (128, 256):
         for b in range(512 // C):
             for m in range(4):
-                for t in range(9):
-                    shift = (t // 3 - 1) * 10 + (t % 3 - 1)
-                    for kc in range(C // 32):
-                        for g in groups:
-                            addrs = [(b * 100 + pad_row(tile[m][lane & 15]) + shift) * pitch
-                                     + (kc * 4 + chunk(lane >> 4)) * 16 for lane in g]
-                            assert len({(a // 16) % 16 for a in addrs}) == 16
+                assert conflict_free(C, [b * stride(C) + pad_row(tile[m][j]) for j in range(16)])
+
+    # edge-row tiling (OAMD_EDGE, edge_tile_row): tile m of position group q is
+    # board row y of boards P and P + NPAIR; SIMD partners (q, q + NPAIR) own
+    # rows 0-3 / 7-4, so tile 0 is row 0 / row 7
+    def edge_tile_row(C, q, m, j):
+        npair = 512 // C // 2
+        P, h = q % npair, q // npair
+        y = 7 - m if h else m
+        r0 = (P * stride(C) + (y + 1) * 10 + 1) & 15
+        oddcol = 1 if (j < 4 or j >= 12) else 0
+        b = P if j < 8 else P + npair
+        x = 2 * (j & 3) + ((r0 & 1) ^ oddcol)
+        return b, y, x, b * stride(C) + (y + 1) * 10 + x + 1
+
+    for C in (128, 256):
+        boards = 512 // C
+        seen = set()
+        for q in range(4 if C == 128 else 2):
+            for m in range(4):
+                sq = [edge_tile_row(C, q, m, j) for j in range(16)]
+                assert conflict_free(C, [r for *_, r in sq])
+                assert len({y for _, y, _, _ in sq}) == 1
+                seen |= {(b, y, x) for b, y, x, _ in sq}
+                if m == 0:  # the skipped tile: rows 0 (taps dy = -1) or 7 (dy = +1)
+                    assert sq[0][1] == (7 if q >= boards // 2 else 0)
+        assert seen == {(b, y, x) for b in range(boards) for y in range(8) for x in range(8)}
 
 
 def test_type_stub_covers_the_reference_surface_and_the_module():

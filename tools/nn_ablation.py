@@ -17,7 +17,8 @@ rows = int(os.environ.get("ROWS", "8192"))
 v = os.environ.get("OAMD_RESNET_ABLATE", "0")
 C = int(os.environ.get("NN_C", "128"))  # 128 -> 128x10b, 256 -> 256x20b
 R = 9 if C == 128 else 19
-net = om.NativeNet(alphazero_state_dict(1, 17, C, R, C), device=0)
+sd = alphazero_state_dict(1, 17, C, R, C)
+net = om.NativeNet(sd, device=0)
 flops = 2.0 * 64 * 9 * C * (17 + 2 * R * C) + 2.0 * (64 * C * 3 + 128 * 65 + 64 * C + C)  # bench.py
 x = (torch.rand((rows, 17, 8, 8), generator=torch.Generator().manual_seed(7)) < 0.3).float().cuda()
 for _ in range(3):
@@ -56,4 +57,10 @@ if ref_file:
         b = torch.load(base_file, weights_only=True)
         chk += (f" [vs baseline max|dp|={(b['policy'] - out['policy'].cpu()).abs().max().item():.2e}"
                 f" max|dv|={(b['value'] - out['value'].cpu()).abs().max().item():.2e}]")
+if os.environ.get("CHECK_REF"):  # accuracy vs the fp32 restatement (oracle/resnet_ref.py), first 256 rows
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import resnet_ref  # noqa: E402
+    ref = resnet_ref.forward(sd, x[:256])
+    chk += (f" [vs fp32: max|dp|={(ref['policy'] - out['policy'][:256]).abs().max().item():.2e}"
+            f" max|dv|={(ref['value'] - out['value'][:256]).abs().max().item():.2e}]")
 print(f"variant {v}: {t:.3f} ms/launch  {flops * rows / t / 1e9:.1f} TFLOP/s  (rows={rows}){chk}", flush=True)
