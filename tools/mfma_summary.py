@@ -5,7 +5,9 @@ Per k_resnet dispatch (averaged):
   clock_GHz   = cycles / kernel-trace duration (MI355X_MICROARCH.md 'DVFS give-back')
   mfma_busy   = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDS x cycles)
   issued_mfma = the kernel's MFMA count (resnet.hip: 128 MFMAs per K-step per
-                4-board workgroup at C=128; ksteps_first + 2R x 36 K-steps)
+                4-board workgroup at C=128; ksteps_first + 2R x 36 K-steps),
+                less the zero-border MFMAs the edge tiling skips at C=128
+                (8 waves x 48 per tower layer and workgroup)
   busy_per_mfma = SQ_VALU_MFMA_BUSY_CYCLES / issued_mfma (16 expected for
                 v_mfma_f32_16x16x32_bf16: the counter's calibration)
   algorithmic = rows x 342.3 MFLOP / duration; frac of the 2.5 PF/s spec peak
@@ -51,6 +53,8 @@ def main(tag: str, args: str = "") -> None:
         ks_first, ks_tower, boards, mfma_per_kstep = 9, 72, 2, 128
     wgs = (rows + boards - 1) // boards
     issued = wgs * mfma_per_kstep * (ks_first + 2 * R * ks_tower)
+    skipped = wgs * 2 * R * 8 * 48 if C == 128 else 0  # OAMD_EDGE (resnet.hip)
+    issued -= skipped
     keys = [k for k in per if k in dur and "GRBM_GUI_ACTIVE" in per[k]]
     n = len(keys)
     avg = lambda f: sum(f(k) for k in keys) / n  # noqa: E731
@@ -71,13 +75,15 @@ def main(tag: str, args: str = "") -> None:
         "SQ_VALU_MFMA_BUSY_CYCLES_per_launch": round(busy),
         "SQ_BUSY_CYCLES_per_launch": round(avg(lambda k: per[k].get("SQ_BUSY_CYCLES", 0.0))),
         "issued_mfma_per_launch": issued,
+        "skipped_zero_border_mfma_per_launch": skipped,
         "busy_per_mfma": round(busy / issued, 3),
         "mfma_busy_frac": round(busy / (SIMDS * cycles), 4),
         "achieved_TFLOPs": round(achieved, 1),
         "frac_of_spec_peak_2.5PF": round(achieved / 2500.0, 4),
         "peak_at_held_clock_TFLOPs": round(SIMDS * FLOP_PER_CLK_SIMD * clock * 1e9 / 1e12, 1),
         "frac_of_peak_at_held_clock": round(achieved / (SIMDS * FLOP_PER_CLK_SIMD * clock * 1e-3), 4),
-        "note": "profiled pass (clocks under rocprofv3 run a few % below un-profiled runs); "
+        "note": "achieved counts the algorithmic FLOPs (skipped zero-border MFMAs included); "
+                "profiled pass (clocks under rocprofv3 run a few % below un-profiled runs); "
                 "GRBM_GUI_ACTIVE summed over 8 XCDs",
     }
     OUT.mkdir(exist_ok=True)
