@@ -153,25 +153,39 @@ static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the 
 #ifndef OAMD_STAGGER
 #define OAMD_STAGGER 0
 #endif
-// Edge-row tiling with zero-tap skipping (throughput geometry, C=128): a
-// 16-position MFMA tile is one board row of two boards, so at the three
-// dy = -1 taps the row-0 tiles (and at dy = +1 the row-7 tiles) read only the
-// zero border and their MFMAs are skipped: 8.3 % of the tower's MFMAs. Waves
-// 0-3 own rows 0-3, their SIMD partners 4-7 rows 7-4. The tower's K order
-// pairs tap a (dy = -1) with tap a + 6 (dy = +1) in one weight stage (same
-// 32-channel block), so every wave skips one of each such stage's two K-steps
-// and the stage barrier stays balanced (kPairOrder; the order is shared by the
-// host packer and every geometry, so all geometries stay bit-identical).
-// The skipped tile's MFMAs are issued last in their K-step, behind a
-// wave-uniform branch (one kernel body). k_resnet_w8, 4096 rows: 0.868-0.872
-// vs 0.887-0.895 ms (two same-box rounds, tools/ab_prebuilt.sh); one body per
-// wave half with compile-time skips measured the same (0.872-0.873, a few
-// spills), and waves 4-7 taking a paired stage's K-steps in swapped order (so
-// every wave skips in the same step) 0.876-0.877: not kept.
+// Edge-row tiling with zero-tap skipping and the dy-sweep K order
+// (throughput geometry, C=128):
+//   * a 16-position MFMA tile is one board row of two boards, so at the three
+//     dy = -1 taps the row-0 tiles (and at dy = +1 the row-7 tiles) read only
+//     the zero border: their MFMAs are skipped (8.3 % of the tower's MFMAs).
+//     Waves 0-3 own rows 0-3, their SIMD partners 4-7 rows 4-7;
+//   * the tower's K order runs, per dx and pair of 32-channel blocks, the
+//     K-steps (cb, dy) = (c,-1) (c,+1) (c,0) (c+1,0) (c+1,-1) (c+1,+1): every
+//     (-1,+1) stage holds one skip for each half, so all waves reach each
+//     stage barrier with the same work, and tile m at dy reads board row
+//     m + dy of its half, so a channel block's 3 taps of one dx read 6
+//     distinct rows, held in a register window: 6 activation-fragment reads
+//     instead of 12;
+//   * the order is one function shared by the host weight packer and every
+//     geometry (the small-batch one reads every fragment), so all geometries
+//     stay bit-identical.
+// k_resnet_w8, 4096 rows, same box: tap-major 0.887-0.895 ms -> pair order
+// (tap a with a + 6 per stage, skips only) 0.868-0.872 -> sweep 0.941 vs 0.996
+// on a slow box (-5.6 %); tools/ab_prebuilt.sh, profiles/r02/.
 #ifndef OAMD_EDGE
 #define OAMD_EDGE 1
 #endif
-__host__ __device__ constexpr bool kPairOrder(int C) { return OAMD_EDGE != 0 && C == 128; }
+__host__ __device__ constexpr bool kSweepOrder(int C) { return OAMD_EDGE != 0 && C == 128; }
+__host__ __device__ constexpr bool kEdgeOrder(int C) { return kSweepOrder(C); }
+// the sweep: (cb, dy) of the J-th K-step of a dx, and the window rows that
+// K-step J needs and no earlier K-step of its channel block has read
+__host__ __device__ constexpr int sweep_cb(int J) { return J / 3; }
+__host__ __device__ constexpr int sweep_dy(int J) {
+    return (J % 6 == 0 || J % 6 == 4) ? -1 : ((J % 6 == 1 || J % 6 == 5) ? 1 : 0);
+}
+__host__ __device__ constexpr int sweep_new(int J) {  // bit i = window row i (board row i - 1 + 4 * half)
+    return J % 6 == 0 ? 0x0F : (J % 6 == 1 ? 0x30 : (J % 6 == 2 ? 0 : (J % 6 == 3 ? 0x1E : (J % 6 == 4 ? 0x01 : 0x20))));
+}
 #ifndef OAMD_PRIO_ALL
 #define OAMD_PRIO_ALL 1  // s_setprio of every ResNet wave, throughput geometry (0 = off)
 #endif
@@ -214,16 +228,14 @@ void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad) {
         *tap = i < 9 ? i : 8;
         *cb = 0;
         *pad = i >= 9;
-    } else if (kPairOrder(C) && i < 6 * (C / 32)) {
-        // stage i/2 = (tap a, block cb), (tap a + 6, block cb)
-        const int pi = i / 2;
-        *tap = pi / (C / 32) + (i & 1) * 6;
-        *cb = pi % (C / 32);
+    } else if (kSweepOrder(C)) {
+        const int dxi = i / 12, J = i % 12;
+        *tap = dxi + 3 * (sweep_dy(J) + 1);
+        *cb = sweep_cb(J);
         *pad = false;
     } else {
-        const int j = kPairOrder(C) ? i - 6 * (C / 32) : i;
-        *tap = (kPairOrder(C) ? 3 : 0) + j / (C / 32);
-        *cb = j % (C / 32);
+        *tap = i / (C / 32);
+        *cb = i % (C / 32);
         *pad = false;
     }
 }
@@ -270,7 +282,7 @@ template <class G>
 __host__ __device__ constexpr int edge_tile_row(int q, int m, int j) {
     constexpr int NP = G::NPAIR > 0 ? G::NPAIR : 1;
     const int P = q % NP, h = q / NP;
-    const int y = h ? 7 - m : m;
+    const int y = 4 * h + m;
     const int r0 = (P * G::BROWS + (y + 1) * 10 + 1) & 15;
     const int oddcol = (j < 4 || j >= 12) ? 1 : 0;
     const int b = j < 8 ? P : P + NP;
@@ -294,9 +306,9 @@ struct GeoT {
     static constexpr int RP = 2 * C + 16;       // row pitch (bytes)
     // board stride in rows (10x10 padded board); with two boards per workgroup
     // 104, so the two boards of an edge tile sit 8 rows apart modulo 16
-    static constexpr int BROWS = BOARDS_ == 2 && kPairOrder(C_) ? 104 : 100;
+    static constexpr int BROWS = BOARDS_ == 2 && kEdgeOrder(C_) ? 104 : 100;
     static constexpr int NPAIR = BOARDS / 2;
-    static constexpr bool EDGE = kPairOrder(C_) && BOARDS >= 2 && BOARDS % 2 == 0 && !OAMD_STAGGER &&
+    static constexpr bool EDGE = kEdgeOrder(C_) && BOARDS >= 2 && BOARDS % 2 == 0 && !OAMD_STAGGER &&
                                  STAGE_ == 2 * 32 * C_ * 2;
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
     static constexpr int KSTEP_BYTES = 32 * C * 2;
@@ -461,12 +473,6 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 template <int DT, int NT>
-__device__ __forceinline__ void mfma_tile0(f32x4_t (&acc)[NT][4], const Frags<NT>& f) {
-#pragma unroll
-    for (int n = 0; n < NT; ++n) acc[n][0] = mfma<DT>(f.w[n], f.x[0], acc[n][0]);
-}
-
-template <int DT, int NT>
 __device__ __forceinline__ void mfma_half(f32x4_t (&acc)[NT][4], const Frags<NT>& f, int h) {
 #pragma unroll
     for (int n = h * NT / 2; n < (h + 1) * NT / 2; ++n)
@@ -474,14 +480,13 @@ __device__ __forceinline__ void mfma_half(f32x4_t (&acc)[NT][4], const Frags<NT>
         for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
 }
 
-// SK: tile 0's MFMAs are left out (edge tiling: issued separately, mfma_tile0)
-template <int DT, bool SK = false, int NT>
+template <int DT, int NT>
 __device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[NT][4], const Frags<NT>& f) {
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
-        for (int m = SK ? 1 : 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
+        for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -904,6 +909,12 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     u32x2_t skip[kNT][4];  // residual (block input) of this lane's outputs
 
     Frags<kNT> fa, fb;
+    // dy-sweep order (G::EDGE && kSweepOrder): activation fragments of the
+    // current / next channel block by window row (fa / fb then carry weights)
+    constexpr bool kSweep = G::EDGE && kSweepOrder(C);
+    u32x4_t win0[6], win1[6];
+    // window base: this lane's column, board row -1 (+ 4 x half), dx = -1
+    const int sb0 = rd[0] - 10 * G::RP - G::RP;
     int g = 0;     // stage holding the current K-step
     int slot = 0;  // g % RING
 
@@ -932,7 +943,6 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         constexpr bool first = kind == 0;
         constexpr int nk = first ? ksteps_first(C) : ksteps_tower(C);
         // edge skipping: which wave half (SIMD partners) this wave is in
-        using RtSkip = std::bool_constant<G::EDGE && !first>;
         const int ehalf = __builtin_amdgcn_readfirstlane(wm / (G::NPAIR > 0 ? G::NPAIR : 1));
 
         // accumulators start at bias (+ block input for the block's second conv)
@@ -957,13 +967,9 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         // of cur's MFMAs go before the barrier, so while waves 0-3 issue the
         // post-barrier DMA and reads, their partners keep the MFMA pipe busy
         // xoff: uniform byte offset of the next K-step's activation rows/channels
-        // RTS (edge tiling): cur's tile-0 MFMAs are issued last, behind a
-        // wave-uniform branch on rsk (tile 0 of cur lies on the zero border)
-        auto step = [&](auto NEW, auto GB, const Frags<kNT>& cur, Frags<kNT>& nxt, int xoff, auto RTS, bool rsk) {
-            constexpr bool rts = decltype(RTS)::value;
+        auto step = [&](auto NEW, auto GB, const Frags<kNT>& cur, Frags<kNT>& nxt, int xoff) {
             constexpr bool open = decltype(NEW)::value;
             constexpr bool gb = decltype(GB)::value;
-            static_assert(!(gb && rts), "stagger without edge skipping");
 #if OAMD_FENCE
             // keep each step's MFMAs (on cur) with the fragment reads they hide:
             // without this fence the scheduler may hoist the next step's MFMAs over
@@ -1050,7 +1056,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             if constexpr (gb) {
                 mfma_half<DT>(acc, cur, 1);
             } else {
-                mfma_frags<DT, rts>(acc, cur);
+                mfma_frags<DT>(acc, cur);
             }
 #if OAMD_READS_FIRST
             // issue the 8 fragment reads first, the stage DMA a few MFMAs later
@@ -1067,14 +1073,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             // fine interleave of the step's fragment reads with its 16 MFMAs: a
             // stage-opening step has the 4 weight reads after the barrier (the
             // activation reads precede it, OAMD_XEARLY), the other step all 8
-            if constexpr (!gb && rts) {
-                constexpr int nds = open && OAMD_XEARLY && !G::EARLY ? 4 : 8;
-                static_for<nds>([&](auto I) {
-                    constexpr int i = decltype(I)::value;
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * 12 / nds - i * 12 / nds, 0);
-                });
-            } else if constexpr (!gb) {
+            if constexpr (!gb) {
                 constexpr int nds = open && OAMD_XEARLY && !G::EARLY ? 4 : 8;
                 if constexpr (OAMD_ILV == 2 && open) __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
                 if constexpr (OAMD_ILV == 5 && open) {  // DMA after the first read + 4 MFMAs
@@ -1104,22 +1103,18 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     __builtin_amdgcn_sched_group_barrier(0x008, kNT * 4 - nds * (OAMD_ILV_SPAN / nds), 0);
             }
 #endif
-            if constexpr (rts) {
-                if (!rsk) mfma_tile0<DT>(acc, cur);
-            }
         };
         using NewOdd = std::integral_constant<bool, G::KS == 1>;  // K-step i1 odd
         using NewEven = std::integral_constant<bool, true>;       // K-step i1 even
-        using NoSkip = std::false_type;
         auto kloop = [&](auto GB) {
             if constexpr (first) {
                 int i = 0;
                 for (; i + 2 < nk; i += 2) {
-                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(i + 1, true), NoSkip{}, false);
-                    step(NewEven{}, GB, fb, fa, kstep_offset<C>(i + 2, true), NoSkip{}, false);
+                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(i + 1, true));
+                    step(NewEven{}, GB, fb, fa, kstep_offset<C>(i + 2, true));
                 }
                 if constexpr (nk % 2 == 0) {
-                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(nk - 1, true), NoSkip{}, false);
+                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(nk - 1, true));
                     mfma_frags<DT>(acc, fb);
                 } else {
                     mfma_frags<DT>(acc, fa);
@@ -1140,35 +1135,113 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                         // the loaded K-step t*KPT + c + 1 opens a stage when it is even
                         using NEW = std::integral_constant<bool, G::KS == 1 || (c + 1) % 2 == 0>;
                         const int xoff = c + 1 == KPT ? tn : to + (c + 1) * 64;
-                        if constexpr (c % 2 == 0) step(NEW{}, GB, fa, fb, xoff, NoSkip{}, false);
-                        else step(NEW{}, GB, fb, fa, xoff, NoSkip{}, false);
+                        if constexpr (c % 2 == 0) step(NEW{}, GB, fa, fb, xoff);
+                        else step(NEW{}, GB, fb, fa, xoff);
                     });
                 };
-                if constexpr (kPairOrder(C)) {
-                    // taps 0-2 paired with 6-8 (stage = (a, cb), (a + 6, cb)), then
-                    // taps 3-5 tap-major. K-step parity <-> fa / fb as before.
-                    static_assert(KPT == 4 && G::KS == 2, "pair order: 2 K-steps per stage");
-                    constexpr int D20 = 20 * G::RP;  // tap a -> a + 6 (dy -1 -> +1)
-                    auto pair_steps = [&](int a, auto LASTA) {
-                        constexpr bool lasta = decltype(LASTA)::value;
-                        const int to = tapoff(a);
-                        const int tn = lasta ? tapoff(3) : to + G::RP;  // tapoff(a + 1), a < 2
-                        static_for<KPT>([&](auto J) {
-                            constexpr int cb = decltype(J)::value;
-                            // cur = (a, cb) in fa: waves 0-3 skip row 0; load (a + 6, cb)
-                            step(std::false_type{}, GB, fa, fb, to + D20 + cb * 64, RtSkip{}, ehalf == 0);
-                            // cur = (a + 6, cb) in fb: waves 4-7 skip row 7; load the next stage
-                            const int xo = cb + 1 < KPT ? to + (cb + 1) * 64 : tn;
-                            step(std::true_type{}, GB, fb, fa, xo, RtSkip{}, ehalf != 0);
+                if constexpr (kSweep) {
+                    static_assert(KPT == 4 && G::KS == 2 && kNT == 4, "sweep: C=128 throughput geometry");
+                    constexpr int RS = 10 * G::RP;  // one board row
+                    // K-step J of the dx at sb (window base + dx): MFMAs from the
+                    // window, weights wc; reads the window rows K-step J + 1 needs
+                    // (at sbn: the next dx's base when J = 11) and its weights
+                    auto sstep = [&](auto JJ, const Frags<kNT>& wc, Frags<kNT>& wn, int sbn) {
+                        constexpr int J = decltype(JJ)::value;
+                        constexpr int Jn = (J + 1) % 12;
+                        constexpr bool open = Jn % 2 == 0;  // K-step J + 1 opens a stage
+                        constexpr int dy = sweep_dy(J), cbn = sweep_cb(Jn), nnew = __builtin_popcount(sweep_new(Jn));
+                        constexpr int tsk = dy < 0 ? 0 : (dy > 0 ? 3 : -1);  // tile on the border for one half
+                        auto& Wc = [&]() -> u32x4_t(&)[6] {
+                            if constexpr (sweep_cb(J) % 2 == 0) return win0; else return win1;
+                        }();
+                        auto& Wn = [&]() -> u32x4_t(&)[6] {
+                            if constexpr (cbn % 2 == 0) return win0; else return win1;
+                        }();
+                        __builtin_amdgcn_sched_barrier(0);
+                        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wc / Wc have landed
+                        // the next K-step's new window rows (do not depend on the barrier)
+                        static_for<6>([&](auto I) {
+                            constexpr int i = decltype(I)::value;
+                            if constexpr ((sweep_new(Jn) >> i) & 1)
+                                Wn[i] = *reinterpret_cast<const u32x4_t*>(act + sbn + i * RS + cbn * 64);
+                        });
+                        if constexpr (open) {
+                            wait_vm<G::VM_OPEN>();
+                            __builtin_amdgcn_s_barrier();
+                            const int sp = (slot + G::AHEAD + 1) % G::RING;
+                            issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
+                            ++g;
+                            slot = slot == G::RING - 1 ? 0 : slot + 1;
+                        } else if constexpr (G::DMA_MODE == 1 || G::DMA_MODE == 3) {
+                            int sa = slot + G::AHEAD;
+                            sa = sa >= G::RING ? sa - G::RING : sa;
+                            issue_stage_dma<G, G::MID_PART>(wsrc, ring, g + G::AHEAD, sa, total, tid);
+                        }
+                        load_wfrags(wn, ring + slot * G::STAGE + (open ? 0 : G::KSTEP_BYTES), wl);
+#pragma unroll
+                        for (int n = 0; n < kNT; ++n)
+#pragma unroll
+                            for (int m = 0; m < 4; ++m)
+                                if (m != tsk) acc[n][m] = mfma<DT>(wc.w[n], Wc[m + 1 + dy], acc[n][m]);
+                        constexpr int nds = open ? kNT : kNT + nnew;
+                        constexpr int nm = kNT * (tsk >= 0 ? 3 : 4);
+                        static_for<nds>([&](auto I) {
+                            constexpr int i = decltype(I)::value;
+                            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                            __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * nm / nds - i * nm / nds, 0);
+                        });
+                        if constexpr (tsk >= 0) {
+                            // waves 0-3 skip tile 0 at dy = -1, waves 4-7 tile 3 at dy = +1
+                            if (dy < 0 ? ehalf != 0 : ehalf == 0)
+#pragma unroll
+                                for (int n = 0; n < kNT; ++n)
+                                    acc[n][tsk] = mfma<DT>(wc.w[n], Wc[tsk + 1 + dy], acc[n][tsk]);
+                        }
+                    };
+                    auto dx_sweep = [&](int dxi, auto LASTDX) {
+                        constexpr bool lastdx = decltype(LASTDX)::value;
+                        const int sb = sb0 + dxi * G::RP;
+                        static_for<lastdx ? 11 : 12>([&](auto JJ) {
+                            constexpr int J = decltype(JJ)::value;
+                            const int sbn = J == 11 ? sb + G::RP : sb;
+                            if constexpr (J % 2 == 0) sstep(JJ, fa, fb, sbn);
+                            else sstep(JJ, fb, fa, sbn);
+                        });
+                        if constexpr (lastdx) {
+                            // K-step 35 = (cb 3, dy +1) in fb / win1: waves 4-7 skip tile 3
+#pragma unroll
+                            for (int n = 0; n < kNT; ++n)
+#pragma unroll
+                                for (int m = 0; m < 3; ++m) acc[n][m] = mfma<DT>(fb.w[n], win1[m + 2], acc[n][m]);
+                            if (ehalf == 0)
+#pragma unroll
+                                for (int n = 0; n < kNT; ++n) acc[n][3] = mfma<DT>(fb.w[n], win1[5], acc[n][3]);
+                        }
+                    };
+#pragma nounroll
+                    for (int dxi = 0; dxi < 2; ++dxi) dx_sweep(dxi, std::false_type{});
+                    dx_sweep(2, std::true_type{});
+                } else if constexpr (kSweepOrder(C)) {
+                    // the sweep order without edge tiles (small-batch geometry):
+                    // generic steps, every K-step's fragments read
+                    static_assert(KPT == 4 && G::KS == 2, "sweep: 2 K-steps per stage");
+                    auto xoff_of = [](int dxi, int J) {
+                        return (sweep_dy(J) * 10 + dxi - 1) * G::RP + sweep_cb(J) * 64;
+                    };
+                    auto dx_steps = [&](int dxi, auto LASTDX) {
+                        constexpr bool lastdx = decltype(LASTDX)::value;
+                        static_for<lastdx ? 11 : 12>([&](auto JJ) {
+                            constexpr int J = decltype(JJ)::value;
+                            using NEW = std::integral_constant<bool, (J + 1) % 2 == 0>;
+                            const int xo = J == 11 ? xoff_of(dxi + 1, 0) : xoff_of(dxi, J + 1);
+                            if constexpr (J % 2 == 0) step(NEW{}, GB, fa, fb, xo);
+                            else step(NEW{}, GB, fb, fa, xo);
                         });
                     };
 #pragma nounroll
-                    for (int a = 0; a < 2; ++a) pair_steps(a, std::false_type{});
-                    pair_steps(2, std::true_type{});
-#pragma nounroll
-                    for (int t = 3; t < 5; ++t) tap_steps(t, std::false_type{});
-                    tap_steps(5, std::true_type{});
-                    mfma_frags<DT>(acc, fb);  // K-step 9*KPT - 1 (odd c)
+                    for (int dxi = 0; dxi < 2; ++dxi) dx_steps(dxi, std::false_type{});
+                    dx_steps(2, std::true_type{});
+                    mfma_frags<DT>(acc, fb);  // K-step 35
                 } else {
                     for (int t = 0; t < 8; ++t) tap_steps(t, std::false_type{});
                     tap_steps(8, std::true_type{});
@@ -1241,8 +1314,14 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 // of the layer already waited for it
                 if constexpr (!OAMD_REGSTAGE && !G::EARLY) wait_vm<G::VM_LAYER>();
                 lds_barrier();           // ... and this layer's output is complete
-                load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false),
-                           rd, wl);
+                if constexpr (kSweep) {
+                    load_wfrags<ABL>(fa, ring + slot * G::STAGE, wl);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
+                } else {
+                    load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false), rd, wl);
+                }
             }
 #ifdef OAMD_STAMPS
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

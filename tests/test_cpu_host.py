@@ -202,12 +202,12 @@ def test_resnet_activation_layout_is_bank_conflict_free():
                 assert conflict_free(C, [b * stride(C) + pad_row(tile[m][j]) for j in range(16)])
 
     # edge-row tiling (OAMD_EDGE, edge_tile_row): tile m of position group q is
-    # board row y of boards P and P + NPAIR; SIMD partners (q, q + NPAIR) own
-    # rows 0-3 / 7-4, so tile 0 is row 0 / row 7
+    # board row y = 4h + m of boards P and P + NPAIR; SIMD partners
+    # (q, q + NPAIR) own rows 0-3 / 4-7, the border tiles are tile 0 / tile 3
     def edge_tile_row(C, q, m, j):
         npair = 512 // C // 2
         P, h = q % npair, q // npair
-        y = 7 - m if h else m
+        y = 4 * h + m
         r0 = (P * stride(C) + (y + 1) * 10 + 1) & 15
         oddcol = 1 if (j < 4 or j >= 12) else 0
         b = P if j < 8 else P + npair
@@ -223,9 +223,45 @@ def test_resnet_activation_layout_is_bank_conflict_free():
                 assert conflict_free(C, [r for *_, r in sq])
                 assert len({y for _, y, _, _ in sq}) == 1
                 seen |= {(b, y, x) for b, y, x, _ in sq}
-                if m == 0:  # the skipped tile: rows 0 (taps dy = -1) or 7 (dy = +1)
-                    assert sq[0][1] == (7 if q >= boards // 2 else 0)
+                assert sq[0][1] == 4 * (q // (boards // 2)) + m  # ascending rows per half
         assert seen == {(b, y, x) for b in range(boards) for y in range(8) for x in range(8)}
+
+
+def test_resnet_sweep_order_window_and_skips():
+    """Restates the tower's dy-sweep K order of csrc/resnet.hip (sweep_cb,
+    sweep_dy, sweep_new; resnet_kstep for C=128) and checks what the kernel
+    relies on: every (tap, 32-channel block) once per layer; each 2-K-step
+    weight stage is either (dy -1, dy +1) of one block, where waves 0-3 skip
+    tile 0 and waves 4-7 tile 3 (one skip each: balanced barriers), or the
+    dy = 0 K-steps of two blocks; and the register window (row i = board row i - 1 of the
+    half) holds every row a K-step reads, each row read once per block and dx
+    and before its first use."""
+    def cb(J):
+        return J // 3
+
+    def dy(J):
+        return -1 if J % 6 in (0, 4) else (1 if J % 6 in (1, 5) else 0)
+
+    new = {0: 0x0F, 1: 0x30, 2: 0, 3: 0x1E, 4: 0x01, 5: 0x20}
+    seq = [(dxi + 3 * (dy(J) + 1), cb(J)) for dxi in range(3) for J in range(12)]
+    assert sorted(seq) == [(t, c) for t in range(9) for c in range(4)]
+    for dxi in range(3):
+        for st in range(6):
+            a, b = 2 * st, 2 * st + 1
+            assert (dy(a), dy(b)) in ((-1, 1), (0, 0))
+            assert dy(a) == 0 or cb(a) == cb(b)
+        held = {}
+        for J in range(12):
+            c = cb(J)
+            loaded = {i for i in range(6) if (new[J % 6] >> i) & 1}
+            assert not (loaded & held.get(c, set()))  # read once per block and dx
+            held.setdefault(c, set()).update(loaded)
+            need = {m + 1 + dy(J) for m in range(4)}
+            assert need <= held[c]
+        assert all(h == set(range(6)) for h in held.values())
+    # the skipped tiles lie on the border: top half tile 0 (row 0) at dy = -1
+    # reads row -1, bottom half tile 3 (row 7) at dy = +1 reads row 8
+    assert 0 + (-1) == -1 and (4 + 3) + 1 == 8
 
 
 def test_type_stub_covers_the_reference_surface_and_the_module():
