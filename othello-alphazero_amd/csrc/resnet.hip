@@ -154,7 +154,7 @@ static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the 
 #define OAMD_STAGGER 0
 #endif
 // Edge-row tiling with zero-tap skipping and the dy-sweep K order
-// (throughput geometry, C=128):
+// (throughput geometries):
 //   * a 16-position MFMA tile is one board row of two boards, so at the three
 //     dy = -1 taps the row-0 tiles (and at dy = +1 the row-7 tiles) read only
 //     the zero border: their MFMAs are skipped (8.3 % of the tower's MFMAs).
@@ -168,14 +168,27 @@ static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the 
 //     instead of 12;
 //   * the order is one function shared by the host weight packer and every
 //     geometry (the small-batch one reads every fragment), so all geometries
-//     stay bit-identical.
+//     stay bit-identical;
+//   * C=256 below (OAMD_SWEEP256).
 // k_resnet_w8, 4096 rows, same box: tap-major 0.887-0.895 ms -> pair order
 // (tap a with a + 6 per stage, skips only) 0.868-0.872 -> sweep 0.941 vs 0.996
 // on a slow box (-5.6 %); tools/ab_prebuilt.sh, profiles/r02/.
 #ifndef OAMD_EDGE
 #define OAMD_EDGE 1
 #endif
-__host__ __device__ constexpr bool kSweepOrder(int C) { return OAMD_EDGE != 0 && C == 128; }
+// C=256 (one K-step per 16 KiB stage, 2 boards per workgroup): the sweep
+// order and window too, and the skips although a stage cannot balance them
+// (each half skips in every other stage): 4096 rows of 256x20b, same box,
+// 7.88-7.93 ms tap-major -> 7.54 sweep -> 7.33 with skips (-7.4 %)
+#ifndef OAMD_SWEEP256
+#define OAMD_SWEEP256 1
+#endif
+#ifndef OAMD_SKIP_KS1
+#define OAMD_SKIP_KS1 1
+#endif
+__host__ __device__ constexpr bool kSweepOrder(int C) {
+    return OAMD_EDGE != 0 && (C == 128 || (C == 256 && OAMD_SWEEP256));
+}
 __host__ __device__ constexpr bool kEdgeOrder(int C) { return kSweepOrder(C); }
 // the sweep: (cb, dy) of the J-th K-step of a dx, and the window rows that
 // K-step J needs and no earlier K-step of its channel block has read
@@ -229,7 +242,7 @@ void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad) {
         *cb = 0;
         *pad = i >= 9;
     } else if (kSweepOrder(C)) {
-        const int dxi = i / 12, J = i % 12;
+        const int dxi = i / (3 * (C / 32)), J = i % (3 * (C / 32));
         *tap = dxi + 3 * (sweep_dy(J) + 1);
         *cb = sweep_cb(J);
         *pad = false;
@@ -309,7 +322,7 @@ struct GeoT {
     static constexpr int BROWS = BOARDS_ == 2 && kEdgeOrder(C_) ? 104 : 100;
     static constexpr int NPAIR = BOARDS / 2;
     static constexpr bool EDGE = kEdgeOrder(C_) && BOARDS >= 2 && BOARDS % 2 == 0 && !OAMD_STAGGER &&
-                                 STAGE_ == 2 * 32 * C_ * 2;
+                                 WC_ == 64 && (STAGE_ == 2 * 32 * C_ * 2 || STAGE_ == 32 * C_ * 2);
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
     static constexpr int KSTEP_BYTES = 32 * C * 2;
     static constexpr int STAGE = STAGE_;
@@ -1140,17 +1153,19 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     });
                 };
                 if constexpr (kSweep) {
-                    static_assert(KPT == 4 && G::KS == 2 && kNT == 4, "sweep: C=128 throughput geometry");
+                    static_assert(kNT == 4 && KPT % 2 == 0 && (G::KS == 1 || G::KS == 2), "sweep geometry");
+                    constexpr int NJ = 3 * KPT;  // K-steps per dx
+                    constexpr bool SKIP = G::KS == 2 || OAMD_SKIP_KS1;
                     constexpr int RS = 10 * G::RP;  // one board row
                     // K-step J of the dx at sb (window base + dx): MFMAs from the
                     // window, weights wc; reads the window rows K-step J + 1 needs
                     // (at sbn: the next dx's base when J = 11) and its weights
                     auto sstep = [&](auto JJ, const Frags<kNT>& wc, Frags<kNT>& wn, int sbn) {
                         constexpr int J = decltype(JJ)::value;
-                        constexpr int Jn = (J + 1) % 12;
-                        constexpr bool open = Jn % 2 == 0;  // K-step J + 1 opens a stage
+                        constexpr int Jn = (J + 1) % NJ;
+                        constexpr bool open = G::KS == 1 || Jn % 2 == 0;  // K-step J + 1 opens a stage
                         constexpr int dy = sweep_dy(J), cbn = sweep_cb(Jn), nnew = __builtin_popcount(sweep_new(Jn));
-                        constexpr int tsk = dy < 0 ? 0 : (dy > 0 ? 3 : -1);  // tile on the border for one half
+                        constexpr int tsk = !SKIP ? -1 : (dy < 0 ? 0 : (dy > 0 ? 3 : -1));  // border tile of one half
                         auto& Wc = [&]() -> u32x4_t(&)[6] {
                             if constexpr (sweep_cb(J) % 2 == 0) return win0; else return win1;
                         }();
@@ -1185,6 +1200,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                                 if (m != tsk) acc[n][m] = mfma<DT>(wc.w[n], Wc[m + 1 + dy], acc[n][m]);
                         constexpr int nds = open ? kNT : kNT + nnew;
                         constexpr int nm = kNT * (tsk >= 0 ? 3 : 4);
+                        // reads spread evenly over the MFMAs (all reads first: +2-3 %)
                         static_for<nds>([&](auto I) {
                             constexpr int i = decltype(I)::value;
                             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -1201,19 +1217,20 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     auto dx_sweep = [&](int dxi, auto LASTDX) {
                         constexpr bool lastdx = decltype(LASTDX)::value;
                         const int sb = sb0 + dxi * G::RP;
-                        static_for<lastdx ? 11 : 12>([&](auto JJ) {
+                        static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
                             constexpr int J = decltype(JJ)::value;
-                            const int sbn = J == 11 ? sb + G::RP : sb;
+                            const int sbn = J == NJ - 1 ? sb + G::RP : sb;
                             if constexpr (J % 2 == 0) sstep(JJ, fa, fb, sbn);
                             else sstep(JJ, fb, fa, sbn);
                         });
                         if constexpr (lastdx) {
-                            // K-step 35 = (cb 3, dy +1) in fb / win1: waves 4-7 skip tile 3
+                            // the layer's last K-step = (last block, dy +1) in fb / win1:
+                            // waves 4-7 skip tile 3
 #pragma unroll
                             for (int n = 0; n < kNT; ++n)
 #pragma unroll
                                 for (int m = 0; m < 3; ++m) acc[n][m] = mfma<DT>(fb.w[n], win1[m + 2], acc[n][m]);
-                            if (ehalf == 0)
+                            if (!SKIP || ehalf == 0)
 #pragma unroll
                                 for (int n = 0; n < kNT; ++n) acc[n][3] = mfma<DT>(fb.w[n], win1[5], acc[n][3]);
                         }
@@ -1224,16 +1241,17 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 } else if constexpr (kSweepOrder(C)) {
                     // the sweep order without edge tiles (small-batch geometry):
                     // generic steps, every K-step's fragments read
-                    static_assert(KPT == 4 && G::KS == 2, "sweep: 2 K-steps per stage");
+                    static_assert(KPT % 2 == 0, "sweep: whole block pairs");
+                    constexpr int NJ = 3 * KPT;
                     auto xoff_of = [](int dxi, int J) {
                         return (sweep_dy(J) * 10 + dxi - 1) * G::RP + sweep_cb(J) * 64;
                     };
                     auto dx_steps = [&](int dxi, auto LASTDX) {
                         constexpr bool lastdx = decltype(LASTDX)::value;
-                        static_for<lastdx ? 11 : 12>([&](auto JJ) {
+                        static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
                             constexpr int J = decltype(JJ)::value;
-                            using NEW = std::integral_constant<bool, (J + 1) % 2 == 0>;
-                            const int xo = J == 11 ? xoff_of(dxi + 1, 0) : xoff_of(dxi, J + 1);
+                            using NEW = std::integral_constant<bool, G::KS == 1 || (J + 1) % 2 == 0>;
+                            const int xo = J == NJ - 1 ? xoff_of(dxi + 1, 0) : xoff_of(dxi, J + 1);
                             if constexpr (J % 2 == 0) step(NEW{}, GB, fa, fb, xo);
                             else step(NEW{}, GB, fb, fa, xo);
                         });
@@ -1241,7 +1259,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 #pragma nounroll
                     for (int dxi = 0; dxi < 2; ++dxi) dx_steps(dxi, std::false_type{});
                     dx_steps(2, std::true_type{});
-                    mfma_frags<DT>(acc, fb);  // K-step 35
+                    mfma_frags<DT>(acc, fb);  // the layer's last K-step
                 } else {
                     for (int t = 0; t < 8; ++t) tap_steps(t, std::false_type{});
                     tap_steps(8, std::true_type{});
@@ -1308,7 +1326,13 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         if (more) {
             if constexpr (wearly) {
                 lds_barrier();  // this layer's output is complete
-                load_xfrags<ABL>(fa, act, kstep_offset<C>(0, false), rd);
+                if constexpr (kSweep) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
+                } else {
+                    load_xfrags<ABL>(fa, act, kstep_offset<C>(0, false), rd);
+                }
             } else {
                 // stage g has landed (later may fly); with EARLY the last barrier
                 // of the layer already waited for it

@@ -243,8 +243,9 @@ def test_resnet_sweep_order_window_and_skips():
         return -1 if J % 6 in (0, 4) else (1 if J % 6 in (1, 5) else 0)
 
     new = {0: 0x0F, 1: 0x30, 2: 0, 3: 0x1E, 4: 0x01, 5: 0x20}
-    seq = [(dxi + 3 * (dy(J) + 1), cb(J)) for dxi in range(3) for J in range(12)]
-    assert sorted(seq) == [(t, c) for t in range(9) for c in range(4)]
+    for nb in (4, 8):  # C = 128, 256: every (tap, block) once per layer
+        seq = [(dxi + 3 * (dy(J) + 1), cb(J)) for dxi in range(3) for J in range(3 * nb)]
+        assert sorted(seq) == [(t, c) for t in range(9) for c in range(nb)]
     for dxi in range(3):
         for st in range(6):
             a, b = 2 * st, 2 * st + 1
