@@ -186,10 +186,34 @@ static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the 
 #ifndef OAMD_SKIP_KS1
 #define OAMD_SKIP_KS1 1
 #endif
-__host__ __device__ constexpr bool kSweepOrder(int C) {
-    return OAMD_EDGE != 0 && (C == 128 || (C == 256 && OAMD_SWEEP256));
+// OAMD_WIDE (C=128): 32-channel x 128-position wave tiles (rows 0-7 of a
+// board pair, 8 MFMA tiles), K order (cb, dy) = (c,-1) (c,0) (c,+1) per dx,
+// an 8-row window: half the weight-fragment reads per MFMA, and every wave
+// skips the same border tiles (0 at dy = -1, 7 at dy = +1) at compile time
+#ifndef OAMD_WIDE
+#define OAMD_WIDE 1
+#endif
+// the same at C=256 (8 waves x 32 channels over both boards of a workgroup)
+#ifndef OAMD_WIDE256
+#define OAMD_WIDE256 1
+#endif
+__host__ __device__ constexpr bool kWideOrder(int C) {
+    return OAMD_EDGE != 0 && ((C == 128 && OAMD_WIDE) || (C == 256 && OAMD_WIDE256));
 }
-__host__ __device__ constexpr bool kEdgeOrder(int C) { return kSweepOrder(C); }
+__host__ __device__ constexpr bool kSweepOrder(int C) {
+    return OAMD_EDGE != 0 && !kWideOrder(C) && (C == 128 || (C == 256 && OAMD_SWEEP256));
+}
+__host__ __device__ constexpr bool kEdgeOrder(int C) { return kSweepOrder(C) || kWideOrder(C); }
+__host__ __device__ constexpr int wide_cb(int J) { return J / 3; }
+__host__ __device__ constexpr int wide_dy(int J) { return J % 3 - 1; }
+// window rows (bit i = board row i - 1) K-step J needs first: rows 0-6 at
+// dy = -1, row 7 at dy = 0
+__host__ __device__ constexpr int wide_new(int J) { return J % 3 == 0 ? 0xFE : (J % 3 == 1 ? 0x100 : 0); }
+// (cb, dy) of K-step J of a dx in the tower's order
+__host__ __device__ constexpr int ord_cb(int C, int J) { return kWideOrder(C) ? wide_cb(J) : J / 3; }
+__host__ __device__ constexpr int ord_dy(int C, int J) {
+    return kWideOrder(C) ? wide_dy(J) : ((J % 6 == 0 || J % 6 == 4) ? -1 : ((J % 6 == 1 || J % 6 == 5) ? 1 : 0));
+}
 // the sweep: (cb, dy) of the J-th K-step of a dx, and the window rows that
 // K-step J needs and no earlier K-step of its channel block has read
 __host__ __device__ constexpr int sweep_cb(int J) { return J / 3; }
@@ -241,10 +265,10 @@ void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad) {
         *tap = i < 9 ? i : 8;
         *cb = 0;
         *pad = i >= 9;
-    } else if (kSweepOrder(C)) {
+    } else if (kSweepOrder(C) || kWideOrder(C)) {
         const int dxi = i / (3 * (C / 32)), J = i % (3 * (C / 32));
-        *tap = dxi + 3 * (sweep_dy(J) + 1);
-        *cb = sweep_cb(J);
+        *tap = dxi + 3 * (ord_dy(C, J) + 1);
+        *cb = ord_cb(C, J);
         *pad = false;
     } else {
         *tap = i / (C / 32);
@@ -307,14 +331,17 @@ __host__ __device__ constexpr int edge_tile_row(int q, int m, int j) {
 // channels per wave (NT = WC/16 MFMA tiles), at most RING_MAX weight slots of
 // STAGE bytes (a whole number of K-steps; the packed weights are K-step
 // granular, so any stage size reads the same buffer).
-template <int C_, int BOARDS_, int WC_, int RING_MAX_, int STAGE_ = stage_bytes<C_>()>
+template <int C_, int BOARDS_, int WC_, int RING_MAX_, int STAGE_ = stage_bytes<C_>(), int PW_ = 64>
 struct GeoT {
     static constexpr int C = C_;
     static constexpr int BOARDS = BOARDS_;
     static constexpr int WC = WC_;
     static constexpr int NT = WC / 16;
     static constexpr int WN = C / WC;           // waves along output channels
-    static constexpr int WAVES = BOARDS * WN;
+    static constexpr int PW = PW_;                      // positions per wave
+    static constexpr int MT = PW / 16;                  // MFMA position tiles per wave
+    static constexpr int WAVES = BOARDS * 64 / PW * WN;
+    static constexpr int WPB = WAVES / BOARDS;          // waves per board (heads)
     static constexpr int THREADS = WAVES * 64;
     static constexpr int RP = 2 * C + 16;       // row pitch (bytes)
     // board stride in rows (10x10 padded board); with two boards per workgroup
@@ -322,7 +349,8 @@ struct GeoT {
     static constexpr int BROWS = BOARDS_ == 2 && kEdgeOrder(C_) ? 104 : 100;
     static constexpr int NPAIR = BOARDS / 2;
     static constexpr bool EDGE = kEdgeOrder(C_) && BOARDS >= 2 && BOARDS % 2 == 0 && !OAMD_STAGGER &&
-                                 WC_ == 64 && (STAGE_ == 2 * 32 * C_ * 2 || STAGE_ == 32 * C_ * 2);
+                                 (kWideOrder(C_) ? (WC_ == 32 && PW_ == 128) : (WC_ == 64 && PW_ == 64)) &&
+                                 (STAGE_ == 2 * 32 * C_ * 2 || STAGE_ == 32 * C_ * 2);
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
     static constexpr int KSTEP_BYTES = 32 * C * 2;
     static constexpr int STAGE = STAGE_;
@@ -359,7 +387,8 @@ struct GeoT {
 };
 // throughput geometry: 512 positions x C channels per workgroup, 8 waves
 template <int C>
-using Geo = GeoT<C, 512 / C, C == 256 ? OAMD_WC256 : OAMD_WC, OAMD_REGSTAGE ? 2 : 3>;
+using Geo = GeoT<C, 512 / C, kWideOrder(C) ? 32 : (C == 256 ? OAMD_WC256 : OAMD_WC), OAMD_REGSTAGE ? 2 : 3,
+                 stage_bytes<C>(), kWideOrder(C) ? 128 : 64>;
 // small-batch geometry (latency): one board per workgroup, 4 waves of C/4
 // channels, so a handful of rows spreads over as many CUs as boards; the LDS
 // ring depth (4, 6 or 8 slots) measured equal: at 8 MFMAs per wave and K-step
@@ -428,10 +457,10 @@ enum InputKind { kPacked = 0, kF32 = 1 };
 
 // Fragments of one K-step: 4 weight tiles (A: 16 channels x 32 K) and
 // 4 activation tiles (B: 32 K x 16 positions).
-template <int NT>
+template <int NT, int MT = 4>
 struct Frags {
     u32x4_t w[NT];
-    u32x4_t x[4];
+    u32x4_t x[MT];
 };
 
 // uniform byte offset of K-step i's rows/channels relative to the lane bases
@@ -451,8 +480,8 @@ __device__ __forceinline__ int kstep_offset(int i, bool first) {
 
 // ds_read the fragments of one K-step: wk = its weights in the ring (uniform),
 // aoff = kstep_offset (uniform); rd[m] / wl are per-lane bases
-template <int ABL = 0, int NT>
-__device__ __forceinline__ void load_wfrags(Frags<NT>& f, const unsigned char* wk, int wl) {
+template <int ABL = 0, int NT, int MT>
+__device__ __forceinline__ void load_wfrags(Frags<NT, MT>& f, const unsigned char* wk, int wl) {
     if constexpr (!(ABL & 4)) {
         const unsigned char* wp = wk + wl;
 #pragma unroll
@@ -460,17 +489,17 @@ __device__ __forceinline__ void load_wfrags(Frags<NT>& f, const unsigned char* w
     }
 }
 
-template <int ABL = 0, int NT>
-__device__ __forceinline__ void load_xfrags(Frags<NT>& f, const unsigned char* act, int aoff, const int (&rd)[4]) {
+template <int ABL = 0, int NT, int MT>
+__device__ __forceinline__ void load_xfrags(Frags<NT, MT>& f, const unsigned char* act, int aoff, const int (&rd)[MT]) {
     if constexpr (ABL & 2) return;
     const unsigned char* ap = act + aoff;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) f.x[m] = *reinterpret_cast<const u32x4_t*>(ap + rd[m]);
+    for (int m = 0; m < MT; ++m) f.x[m] = *reinterpret_cast<const u32x4_t*>(ap + rd[m]);
 }
 
-template <int ABL = 0, int NT>
-__device__ __forceinline__ void load_frags(Frags<NT>& f, const unsigned char* act, const unsigned char* wk,
-                                           int aoff, const int (&rd)[4], int wl) {
+template <int ABL = 0, int NT, int MT>
+__device__ __forceinline__ void load_frags(Frags<NT, MT>& f, const unsigned char* act, const unsigned char* wk,
+                                           int aoff, const int (&rd)[MT], int wl) {
     load_wfrags<ABL>(f, wk, wl);
     load_xfrags<ABL>(f, act, aoff, rd);
 }
@@ -485,21 +514,21 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-template <int DT, int NT>
-__device__ __forceinline__ void mfma_half(f32x4_t (&acc)[NT][4], const Frags<NT>& f, int h) {
+template <int DT, int NT, int MT>
+__device__ __forceinline__ void mfma_half(f32x4_t (&acc)[NT][MT], const Frags<NT, MT>& f, int h) {
 #pragma unroll
     for (int n = h * NT / 2; n < (h + 1) * NT / 2; ++n)
 #pragma unroll
-        for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
+        for (int m = 0; m < MT; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
 }
 
-template <int DT, int NT>
-__device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[NT][4], const Frags<NT>& f) {
+template <int DT, int NT, int MT>
+__device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[NT][MT], const Frags<NT, MT>& f) {
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
-        for (int m = 0; m < 4; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
+        for (int m = 0; m < MT; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
     if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -666,14 +695,14 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
     const int ntask = 4 + 2 * nvs;
     float wv[32];
     // waves without phase-1 work issue their first task's weights now
-    if (wave % G::WN != 0 && wave < ntask) task_weights(wave, wv);
+    if (wave % G::WPB != 0 && wave < ntask) task_weights(wave, wv);
     OAMD_STAMP(8);
     // phase 1: both 1x1 convs of a board as one small MFMA GEMM on the wave
     // that owns the board's first channel block: A = folded head conv weights
     // (rows 0, 1 = policy channels, row 2 = value, rows 3-15 zero; packed in
     // fragment order on the host), B = the tower output at the centre tap.
-    if (wave % G::WN == 0) {
-        const int b = wave / G::WN;
+    if (wave % G::WPB == 0) {
+        const int b = wave / G::WPB;
         u32x4_t hw[C / 32];
 #pragma unroll
         for (int cb = 0; cb < C / 32; ++cb)
@@ -707,7 +736,7 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
         float acc[B];
 #pragma unroll
         for (int b = 0; b < B; ++b) acc[b] = 0.0f;
-        if (task != wave || wave % G::WN == 0) task_weights(task, wv);
+        if (task != wave || wave % G::WPB == 0) task_weights(task, wv);
         if (task < 4) {  // policy Linear(128->64 of 65), inputs 32*task ..
             const float* x = sp + task * 32 * B;
             dot32<B>(acc, wv, x);
@@ -786,6 +815,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                                             float* __restrict__ policy, float* __restrict__ value) {
     constexpr int C = G::C;
     constexpr int kNT = G::NT;
+    constexpr int kMT = G::MT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* act = smem;
     unsigned char* ring = smem + G::ACT_BYTES;
@@ -842,9 +872,9 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 
     // per-lane bases: fragment reads (row of position tile m + k-group chunk),
     // epilogue writes (row + k-group's 8-byte half chunk), weight fragments
-    int rd[4], wr[4];
+    int rd[kMT], wr[kMT];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < kMT; ++m) {
         const int rowb = (G::EDGE ? edge_tile_row<G>(wm, m, lane & 15)
                                   : wm * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) *
                          G::RP;
@@ -918,14 +948,15 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 u32x4_t{words[4 * c], words[4 * c + 1], words[4 * c + 2], words[4 * c + 3]};
     }
 
-    f32x4_t acc[kNT][4];
-    u32x2_t skip[kNT][4];  // residual (block input) of this lane's outputs
+    f32x4_t acc[kNT][kMT];
+    u32x2_t skip[kNT][kMT];  // residual (block input) of this lane's outputs
 
-    Frags<kNT> fa, fb;
+    Frags<kNT, kMT> fa, fb;
     // dy-sweep order (G::EDGE && kSweepOrder): activation fragments of the
     // current / next channel block by window row (fa / fb then carry weights)
     constexpr bool kSweep = G::EDGE && kSweepOrder(C);
-    u32x4_t win0[6], win1[6];
+    constexpr bool kWide = G::EDGE && kWideOrder(C);
+    u32x4_t win0[kWide ? 9 : 6], win1[kWide ? 9 : 6];
     // window base: this lane's column, board row -1 (+ 4 x half), dx = -1
     const int sb0 = rd[0] - 10 * G::RP - G::RP;
     int g = 0;     // stage holding the current K-step
@@ -962,7 +993,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 #pragma unroll
         for (int n = 0; n < kNT; ++n)
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
+            for (int m = 0; m < kMT; ++m) {
                 f32x4_t a = f32x4_t{bv[n].x, bv[n].y, bv[n].z, bv[n].w};
                 if constexpr (kind == 2) {
                     const u32x2_t r = skip[n][m];
@@ -980,7 +1011,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         // of cur's MFMAs go before the barrier, so while waves 0-3 issue the
         // post-barrier DMA and reads, their partners keep the MFMA pipe busy
         // xoff: uniform byte offset of the next K-step's activation rows/channels
-        auto step = [&](auto NEW, auto GB, const Frags<kNT>& cur, Frags<kNT>& nxt, int xoff) {
+        auto step = [&](auto NEW, auto GB, const Frags<kNT, kMT>& cur, Frags<kNT, kMT>& nxt, int xoff) {
             constexpr bool open = decltype(NEW)::value;
             constexpr bool gb = decltype(GB)::value;
 #if OAMD_FENCE
@@ -1086,7 +1117,16 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             // fine interleave of the step's fragment reads with its 16 MFMAs: a
             // stage-opening step has the 4 weight reads after the barrier (the
             // activation reads precede it, OAMD_XEARLY), the other step all 8
-            if constexpr (!gb) {
+            if constexpr (!gb && kMT != 4) {
+                // other tile counts: the step's reads spread evenly over its MFMAs
+                constexpr int nds = open && OAMD_XEARLY && !G::EARLY ? kNT : kNT + kMT;
+                constexpr int nm = kNT * kMT;
+                static_for<nds>([&](auto I) {
+                    constexpr int i = decltype(I)::value;
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * nm / nds - i * nm / nds, 0);
+                });
+            } else if constexpr (!gb) {
                 constexpr int nds = open && OAMD_XEARLY && !G::EARLY ? 4 : 8;
                 if constexpr (OAMD_ILV == 2 && open) __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
                 if constexpr (OAMD_ILV == 5 && open) {  // DMA after the first read + 4 MFMAs
@@ -1152,7 +1192,78 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                         else step(NEW{}, GB, fb, fa, xoff);
                     });
                 };
-                if constexpr (kSweep) {
+                if constexpr (kWide) {
+                    static_assert(kNT == 2 && kMT == 8 && KPT % 2 == 0 && (G::KS == 1 || G::KS == 2), "wide geometry");
+                    constexpr int NJ = 3 * KPT;  // K-steps per dx
+                    constexpr int RS = 10 * G::RP;  // one board row
+                    // K-step J = (cb J/3, dy J%3 - 1) of the dx: tiles mlo..mhi-1
+                    // from window rows m + 1 + dy (tile 0 at dy = -1 and tile 7 at
+                    // dy = +1 read the zero border: left out, every wave alike)
+                    auto wstep = [&](auto JJ, const Frags<kNT, kMT>& wc, Frags<kNT, kMT>& wn, int sbn) {
+                        constexpr int J = decltype(JJ)::value;
+                        constexpr int Jn = (J + 1) % NJ;
+                        constexpr bool open = G::KS == 1 || Jn % 2 == 0;
+                        constexpr int dy = wide_dy(J), cbn = wide_cb(Jn), nnew = __builtin_popcount(wide_new(Jn));
+                        constexpr int mlo = dy < 0 ? 1 : 0, mhi = dy > 0 ? 7 : 8;
+                        auto& Wc = [&]() -> u32x4_t(&)[9] {
+                            if constexpr (wide_cb(J) % 2 == 0) return win0; else return win1;
+                        }();
+                        auto& Wn = [&]() -> u32x4_t(&)[9] {
+                            if constexpr (cbn % 2 == 0) return win0; else return win1;
+                        }();
+                        __builtin_amdgcn_sched_barrier(0);
+                        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wc / Wc have landed
+                        static_for<9>([&](auto I) {
+                            constexpr int i = decltype(I)::value;
+                            if constexpr ((wide_new(Jn) >> i) & 1)
+                                Wn[i] = *reinterpret_cast<const u32x4_t*>(act + sbn + i * RS + cbn * 64);
+                        });
+                        if constexpr (open) {
+                            wait_vm<G::VM_OPEN>();
+                            __builtin_amdgcn_s_barrier();
+                            const int sp = (slot + G::AHEAD + 1) % G::RING;
+                            issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
+                            ++g;
+                            slot = slot == G::RING - 1 ? 0 : slot + 1;
+                        } else if constexpr (G::DMA_MODE == 1 || G::DMA_MODE == 3) {
+                            int sa = slot + G::AHEAD;
+                            sa = sa >= G::RING ? sa - G::RING : sa;
+                            issue_stage_dma<G, G::MID_PART>(wsrc, ring, g + G::AHEAD, sa, total, tid);
+                        }
+                        load_wfrags(wn, ring + slot * G::STAGE + (open ? 0 : G::KSTEP_BYTES), wl);
+#pragma unroll
+                        for (int n = 0; n < kNT; ++n)
+#pragma unroll
+                            for (int m = mlo; m < mhi; ++m) acc[n][m] = mfma<DT>(wc.w[n], Wc[m + 1 + dy], acc[n][m]);
+                        constexpr int nds = open ? kNT : kNT + nnew;
+                        constexpr int nm = kNT * (mhi - mlo);
+                        static_for<nds>([&](auto I) {
+                            constexpr int i = decltype(I)::value;
+                            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                            __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * nm / nds - i * nm / nds, 0);
+                        });
+                    };
+                    auto dx_wide = [&](int dxi, auto LASTDX) {
+                        constexpr bool lastdx = decltype(LASTDX)::value;
+                        const int sb = sb0 + dxi * G::RP;
+                        static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
+                            constexpr int J = decltype(JJ)::value;
+                            const int sbn = J == NJ - 1 ? sb + G::RP : sb;
+                            if constexpr (J % 2 == 0) wstep(JJ, fa, fb, sbn);
+                            else wstep(JJ, fb, fa, sbn);
+                        });
+                        if constexpr (lastdx) {
+                            // the layer's last K-step = (last block, dy +1) in fb / win1
+#pragma unroll
+                            for (int n = 0; n < kNT; ++n)
+#pragma unroll
+                                for (int m = 0; m < 7; ++m) acc[n][m] = mfma<DT>(fb.w[n], win1[m + 2], acc[n][m]);
+                        }
+                    };
+#pragma nounroll
+                    for (int dxi = 0; dxi < 2; ++dxi) dx_wide(dxi, std::false_type{});
+                    dx_wide(2, std::true_type{});
+                } else if constexpr (kSweep) {
                     static_assert(kNT == 4 && KPT % 2 == 0 && (G::KS == 1 || G::KS == 2), "sweep geometry");
                     constexpr int NJ = 3 * KPT;  // K-steps per dx
                     constexpr bool SKIP = G::KS == 2 || OAMD_SKIP_KS1;
@@ -1160,7 +1271,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     // K-step J of the dx at sb (window base + dx): MFMAs from the
                     // window, weights wc; reads the window rows K-step J + 1 needs
                     // (at sbn: the next dx's base when J = 11) and its weights
-                    auto sstep = [&](auto JJ, const Frags<kNT>& wc, Frags<kNT>& wn, int sbn) {
+                    auto sstep = [&](auto JJ, const Frags<kNT, kMT>& wc, Frags<kNT, kMT>& wn, int sbn) {
                         constexpr int J = decltype(JJ)::value;
                         constexpr int Jn = (J + 1) % NJ;
                         constexpr bool open = G::KS == 1 || Jn % 2 == 0;  // K-step J + 1 opens a stage
@@ -1238,13 +1349,13 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 #pragma nounroll
                     for (int dxi = 0; dxi < 2; ++dxi) dx_sweep(dxi, std::false_type{});
                     dx_sweep(2, std::true_type{});
-                } else if constexpr (kSweepOrder(C)) {
-                    // the sweep order without edge tiles (small-batch geometry):
+                } else if constexpr (kSweepOrder(C) || kWideOrder(C)) {
+                    // the tower's order without edge tiles (small-batch geometry):
                     // generic steps, every K-step's fragments read
                     static_assert(KPT % 2 == 0, "sweep: whole block pairs");
                     constexpr int NJ = 3 * KPT;
                     auto xoff_of = [](int dxi, int J) {
-                        return (sweep_dy(J) * 10 + dxi - 1) * G::RP + sweep_cb(J) * 64;
+                        return (ord_dy(C, J) * 10 + dxi - 1) * G::RP + ord_cb(C, J) * 64;
                     };
                     auto dx_steps = [&](int dxi, auto LASTDX) {
                         constexpr bool lastdx = decltype(LASTDX)::value;
@@ -1313,7 +1424,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 #pragma unroll
         for (int n = 0; n < kNT; ++n)
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
+            for (int m = 0; m < kMT; ++m) {
                 if constexpr (ABL & 16) continue;
                 u32x2_t* p = reinterpret_cast<u32x2_t*>(act + wr[m] + n * 32);
                 if constexpr (kind == 1) skip[n][m] = *p;  // block input, needed by conv2
@@ -1330,6 +1441,10 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
+                } else if constexpr (kWide) {
+#pragma unroll
+                    for (int i = 1; i < 8; ++i)
+                        win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
                 } else {
                     load_xfrags<ABL>(fa, act, kstep_offset<C>(0, false), rd);
                 }
@@ -1342,6 +1457,11 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     load_wfrags<ABL>(fa, ring + slot * G::STAGE, wl);
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
+                        win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
+                } else if constexpr (kWide) {
+                    load_wfrags<ABL>(fa, ring + slot * G::STAGE, wl);
+#pragma unroll
+                    for (int i = 1; i < 8; ++i)
                         win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
                 } else {
                     load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false), rd, wl);

@@ -202,8 +202,9 @@ def test_resnet_activation_layout_is_bank_conflict_free():
                 assert conflict_free(C, [b * stride(C) + pad_row(tile[m][j]) for j in range(16)])
 
     # edge-row tiling (OAMD_EDGE, edge_tile_row): tile m of position group q is
-    # board row y = 4h + m of boards P and P + NPAIR; SIMD partners
-    # (q, q + NPAIR) own rows 0-3 / 4-7, the border tiles are tile 0 / tile 3
+    # board row y = 4h + m of boards P and P + NPAIR. 64-position waves (PW 64,
+    # the OAMD_WIDE=0 alternative): SIMD partners (q, q + NPAIR) own rows 0-3 /
+    # 4-7; 128-position waves (PW 128, OAMD_WIDE, the default): rows 0-7
     def edge_tile_row(C, q, m, j):
         npair = 512 // C // 2
         P, h = q % npair, q // npair
@@ -216,15 +217,51 @@ def test_resnet_activation_layout_is_bank_conflict_free():
 
     for C in (128, 256):
         boards = 512 // C
-        seen = set()
-        for q in range(4 if C == 128 else 2):
-            for m in range(4):
-                sq = [edge_tile_row(C, q, m, j) for j in range(16)]
-                assert conflict_free(C, [r for *_, r in sq])
-                assert len({y for _, y, _, _ in sq}) == 1
-                seen |= {(b, y, x) for b, y, x, _ in sq}
-                assert sq[0][1] == 4 * (q // (boards // 2)) + m  # ascending rows per half
-        assert seen == {(b, y, x) for b in range(boards) for y in range(8) for x in range(8)}
+        for pw in (64, 128):
+            seen = set()
+            for q in range(boards * 64 // pw):
+                for m in range(pw // 16):
+                    sq = [edge_tile_row(C, q, m, j) for j in range(16)]
+                    assert conflict_free(C, [r for *_, r in sq])
+                    assert len({y for _, y, _, _ in sq}) == 1
+                    seen |= {(b, y, x) for b, y, x, _ in sq}
+                    assert sq[0][1] == 4 * (q // (boards // 2)) + m  # ascending rows
+                    # one column map for all rows of a wave: the register window
+                    # reads row r of the wave as base + r board rows
+                    r0 = [edge_tile_row(C, q, 0, j)[3] for j in range(16)]
+                    assert [r - 10 * m for *_, r in sq] == r0
+            assert seen == {(b, y, x) for b in range(boards) for y in range(8) for x in range(8)}
+
+
+def test_resnet_wide_order_window_and_skips():
+    """The default tower order of csrc/resnet.hip (OAMD_WIDE: wide_cb, wide_dy,
+    wide_new; resnet_kstep): per dx and 32-channel block the K-steps dy = -1,
+    0, +1. Every (tap, block) once per layer; 128-position waves own rows 0-7,
+    so every wave leaves out tile 0 at dy = -1 (row -1) and tile 7 at dy = +1
+    (row 8), the same MFMAs in every wave; the 8-row window (row i = board row
+    i - 1, rows 1-8 only) holds every row a K-step reads, each read once per
+    block and dx, before its first use."""
+    def cb(J):
+        return J // 3
+
+    def dy(J):
+        return J % 3 - 1
+
+    new = {0: 0xFE, 1: 0x100, 2: 0}
+    for nb in (4, 8):
+        seq = [(dxi + 3 * (dy(J) + 1), cb(J)) for dxi in range(3) for J in range(3 * nb)]
+        assert sorted(seq) == [(t, c) for t in range(9) for c in range(nb)]
+        held = {}
+        for J in range(3 * nb):
+            loaded = {i for i in range(9) if (new[J % 3] >> i) & 1}
+            assert not (loaded & held.get(cb(J), set()))
+            held.setdefault(cb(J), set()).update(loaded)
+            tiles = range(1 if dy(J) < 0 else 0, 7 if dy(J) > 0 else 8)
+            need = {m + 1 + dy(J) for m in tiles}
+            assert need <= held[cb(J)]
+            skipped = set(range(8)) - set(tiles)
+            assert all(m + dy(J) in (-1, 8) for m in skipped)  # border rows only
+        assert all(h == set(range(1, 9)) for h in held.values())
 
 
 def test_resnet_sweep_order_window_and_skips():
