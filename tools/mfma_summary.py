@@ -6,8 +6,8 @@ Per k_resnet dispatch (averaged):
   mfma_busy   = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDS x cycles)
   issued_mfma = the kernel's MFMA count (resnet.hip: 128 MFMAs per K-step per
                 4-board workgroup at C=128; ksteps_first + 2R x 36 K-steps),
-                less the zero-border MFMAs the edge tiling skips at C=128
-                (8 waves x 48 per tower layer and workgroup)
+                less the zero-border MFMAs the edge tiling skips (8 waves x 48
+                per tower layer and workgroup at C=128, x 96 at C=256)
   busy_per_mfma = SQ_VALU_MFMA_BUSY_CYCLES / issued_mfma (16 expected for
                 v_mfma_f32_16x16x32_bf16: the counter's calibration)
   algorithmic = rows x 342.3 MFLOP / duration; frac of the 2.5 PF/s spec peak
@@ -53,7 +53,9 @@ def main(tag: str, args: str = "") -> None:
         ks_first, ks_tower, boards, mfma_per_kstep = 9, 72, 2, 128
     wgs = (rows + boards - 1) // boards
     issued = wgs * mfma_per_kstep * (ks_first + 2 * R * ks_tower)
-    skipped = wgs * 2 * R * 8 * 48 if C == 128 else 0  # OAMD_EDGE (resnet.hip)
+    # OAMD_EDGE (resnet.hip): per tower layer every wave leaves out 8.3 % of its
+    # MFMAs (C=128: 48 of 576, C=256: 96 of 1152), 8 waves per workgroup
+    skipped = wgs * 2 * R * 8 * (48 if C == 128 else 96)
     issued -= skipped
     keys = [k for k in per if k in dur and "GRBM_GUI_ACTIVE" in per[k]]
     n = len(keys)
