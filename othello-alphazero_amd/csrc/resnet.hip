@@ -9,7 +9,9 @@
 //     K = 9 taps x C_in, on v_mfma_f32_16x16x32_{bf16,f16} with the WEIGHTS as
 //     the A operand: an accumulator lane then holds 4 consecutive output
 //     channels of one position, so the epilogue writes 8 contiguous bytes;
-//     wave (wm, wn) owns 64 channels (wn) x the 64 positions of board wm;
+//     throughput geometries: wave (wm, wn) owns 32 channels (wn) x rows 0-7
+//     of board pair wm (OAMD_WIDE, edge tiling below); small-batch geometry:
+//     C/8 channels x the 64 positions of the board;
 //   * K is walked in K-steps of one tap x 32 input channels. Weights (BatchNorm
 //     folded, packed on the host in fragment order) stream once per workgroup
 //     through a 3-slot LDS ring by LDS-DMA (global_load_lds_dwordx4); a 16 KiB
