@@ -54,7 +54,7 @@ def test_native_net_vs_reference_golden(om, golden_dir, name, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
-@pytest.mark.parametrize("rows", [1, 3, 4, 5, 257, 2048])
+@pytest.mark.parametrize("rows", [1, 3, 4, 5, 257, 1027, 2048])
 def test_native_net_vs_torch_fp32_restatement(om, rows, dtype):
     """Ragged batch sizes (partial last workgroup tile) on real-looking planes."""
     from othello_mcts.synthetic import alphazero_state_dict
@@ -235,13 +235,17 @@ def test_nn_batch_does_not_change_results(om):
 def test_small_batch_geometry_is_bit_identical(om, dtype, C, R):
     """Fewer than 1024 rows run one board per workgroup (latency geometry);
     the K order per output is unchanged, so rows evaluated alone match the
-    same rows inside a large (throughput-geometry) batch bit for bit."""
+    same rows inside a large (throughput-geometry) batch bit for bit. 1101
+    rows: the large batch's last workgroup is ragged (1101 = 4 x 275 + 1)."""
     from othello_mcts.synthetic import alphazero_state_dict
 
     net = om.NativeNet(alphazero_state_dict(11, 17, C, R, 64), device=0, dtype=dtype)
     gen = torch.Generator().manual_seed(C)
-    x = (torch.rand((1100, 17, 8, 8), generator=gen) < 0.3).float().to(DEV)
+    x = (torch.rand((1101, 17, 8, 8), generator=gen) < 0.3).float().to(DEV)
     big = net(x)
     small = net(x[:100].contiguous())
     assert torch.equal(big["policy"][:100], small["policy"])
     assert torch.equal(big["value"][:100], small["value"])
+    tail = net(x[1001:].contiguous())  # the ragged last workgroup's board, alone
+    assert torch.equal(big["policy"][1001:], tail["policy"])
+    assert torch.equal(big["value"][1001:], tail["value"])
