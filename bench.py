@@ -1,9 +1,13 @@
 """Benchmark: whole-node MCTS simulations/sec, 800 sims/move, 128x10b ResNet.
 
 BASELINE.json metric on configs[1] (256 concurrent self-play games, 128x10b,
-bf16, one MI355X) per GPU; with --gpus N (torchrun, one process per GPU) every
-rank runs its own 256 games (games shard embarrassingly: no collective on the
-hot path, "scaling": "weak").
+bf16, one MI355X) per GPU. With --gpus N every rank (one process per GPU)
+runs its own 256 games: games shard embarrassingly, no collective on the hot
+path, "scaling": "weak". The rank processes come from the driver's
+torch.distributed.run, or, when bench.py is started bare with --gpus N > 1,
+from a torch.distributed.run child that bench.py starts itself before it
+touches the GPU. A run whose ranks do not match --gpus, or whose ranks share
+GPUs without the explicit gloo rehearsal (OAMD_BENCH_BACKEND=gloo), fails.
 
 A step is one self-play move of every game on the GPU: a full 800-simulation
 search (25 steps of select -> fused ResNet -> expand/backup for T=2 x B=16
@@ -14,11 +18,17 @@ Synthetic data: random-init AlphaZeroNet weights of the 128x10b architecture
 
 Also reported (rank 0):
   roofline      the fused ResNet kernel: algorithmic FLOPs (342.3 MFLOP per
-                evaluated leaf) / its average HIP-event duration, vs the
-                2.5 PFLOP/s dense bf16 MFMA peak; traffic from profiles/ if a
-                PMC summary for this config exists, else null.
+                evaluated leaf, n_eval = rows of non-terminal leaves,
+                BASELINE.md) / its average HIP-event duration, vs the 2.5
+                PFLOP/s dense bf16 MFMA peak; traffic from profiles/ if a PMC
+                summary for this config exists, else null.
   cpu_baseline  the oracle C restatement of the reference search + torch-CPU
-                fp32 ResNet, 1 game (configs[0]), bounded sample on this host.
+                fp32 ResNet, 1 game (configs[0]), a fixed number of moves after
+                a fixed warm-up, torch threads = the CPUs this process may use.
+
+--dry-run exercises the rank plumbing (launch, checks, barrier-bracketed
+max-over-ranks timing, rank table, aggregation, the JSON line) with no GPU and
+no search: gloo on the CPU, every step a fixed sleep. Its line says so.
 """
 
 from __future__ import annotations
@@ -26,6 +36,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -36,6 +48,7 @@ sys.path.insert(0, str(ROOT / "othello-alphazero_amd"))
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+METRIC = "MCTS simulations/sec (whole node), 800 sims/move, 128x10b ResNet, 1/2/4/8 GPU"
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0}  # MI355X dense MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 # BASELINE.md "Published numbers for this path": the reference on 1x RTX 4090 +
@@ -50,13 +63,38 @@ def resnet_flops_per_eval(in_ch: int, C: int, R: int, hidden: int) -> float:
     return float(conv0 + tower + heads)
 
 
-def cpu_baseline(seconds: float, history: int, C: int, R: int, hidden: int, max_moves: int | None = None,
-                 warmup_moves: int = 0) -> dict:
-    """Oracle port of the reference CPU path (configs[0]): 1 game, 2 threads x 16,
-    800 sims/move, fp32 torch-CPU ResNet; moves until `seconds` elapse (or
-    `max_moves`), after `warmup_moves` untimed moves. Validated against the
-    compiled reference in the build container: tools/cpu_baseline_validate.py,
-    profiles/r02_cpu_baseline_validation.json."""
+# ---- CPU baseline (configs[0]) ----------------------------------------------
+
+def usable_cpus() -> dict:
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2
+    CPU quota (a GPU box grants a share of a larger machine; os.cpu_count()
+    shows the whole machine)."""
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = nproc
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        quota = None
+    usable = min(affinity, quota) if quota else affinity
+    return {"nproc": nproc, "affinity_cpus": affinity, "cgroup_quota_cpus": quota, "usable": usable}
+
+
+def cpu_baseline(history: int, C: int, R: int, hidden: int, moves: int = 24, warmup_moves: int = 2,
+                 threads: int | None = None, max_seconds: float = 120.0) -> dict:
+    """Oracle port of the reference CPU path (configs[0]): 1 game from the
+    initial position, 2 threads x 16, 800 sims/move, eps 0.25, fp32 torch-CPU
+    ResNet; `warmup_moves` untimed moves, then `moves` timed ones (stopping
+    early only past `max_seconds`). The game is fixed by its random-stream key,
+    so every box times the same positions. torch intra-op threads = `threads`
+    (default: every CPU this process may use, BASELINE.md "CPU-baseline
+    plan"). Validated against the compiled reference in the build container:
+    tools/cpu_baseline_validate.py, profiles/r03_cpu_baseline_validation.json."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
 
@@ -64,38 +102,48 @@ def cpu_baseline(seconds: float, history: int, C: int, R: int, hidden: int, max_
     import resnet_ref
     from othello_mcts.synthetic import alphazero_state_dict
 
-    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
-          alphazero_state_dict(1, 1 + 2 * history, C, R, hidden).items()}
+    cpus = usable_cpus()
+    if threads is None:
+        threads = cpus["usable"]
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
+              alphazero_state_dict(1, 1 + 2 * history, C, R, hidden).items()}
 
-    def nn(feat):
-        with torch.no_grad():
-            out = resnet_ref.forward(sd, torch.from_numpy(np.ascontiguousarray(feat)))
-        return out["policy"].numpy(), out["value"].numpy()
+        def nn(feat):
+            with torch.no_grad():
+                out = resnet_ref.forward(sd, torch.from_numpy(np.ascontiguousarray(feat)))
+            return out["policy"].numpy(), out["value"].numpy()
 
-    m = O.OracleMCTS(history_size=history, num_simulations=800, num_threads=2, batch_size=16,
-                     dirichlet_epsilon=0.25, game_key=5)
-    def move():
-        if m.position().player == 0:
-            m.reset_position()
-        n = m.search(nn)
-        vc = m.visit_counts()
-        m.apply_action(O.legal_actions(m.position())[int(np.argmax(vc))])
-        return n
+        m = O.OracleMCTS(history_size=history, num_simulations=800, num_threads=2, batch_size=16,
+                         dirichlet_epsilon=0.25, game_key=5)
 
-    for _ in range(warmup_moves):
-        move()
-    sims = 0
-    moves = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds and (max_moves is None or moves < max_moves):
-        sims += move()
-        moves += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(sims / dt, 1), "unit": "simulations/s", "cores": torch.get_num_threads(),
-            "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-            "affinity_cpus": len(os.sched_getaffinity(0)),
-            "sample": f"1 game from the initial position, {moves} moves x 800 sims (T=2 x B=16, "
-                      f"eps=0.25), {C}x{R + 1}b fp32 torch-CPU, {dt:.1f} s"}
+        def move():
+            if m.position().player == 0:
+                m.reset_position()
+            n = m.search(nn)
+            vc = m.visit_counts()
+            m.apply_action(O.legal_actions(m.position())[int(np.argmax(vc))])
+            return n
+
+        for _ in range(warmup_moves):
+            move()
+        sims = 0
+        done = 0
+        t0 = time.perf_counter()
+        while done < moves and time.perf_counter() - t0 < max_seconds:
+            sims += move()
+            done += 1
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev_threads)
+    return {"value": round(sims / dt, 1), "unit": "simulations/s", "cores": cpus["usable"], "threads": threads,
+            "kind": "port", "cpu_model": cpu_model(), "nproc": cpus["nproc"],
+            "affinity_cpus": cpus["affinity_cpus"], "cgroup_quota_cpus": cpus["cgroup_quota_cpus"],
+            "moves": done, "warmup_moves": warmup_moves,
+            "sample": f"1 game from the initial position, {warmup_moves} warm-up + {done} timed moves x 800 sims "
+                      f"(T=2 x B=16, eps=0.25), {C}x{R + 1}b fp32 torch-CPU with {threads} threads, {dt:.1f} s"}
 
 
 def cpu_model() -> str:
@@ -109,12 +157,16 @@ def cpu_model() -> str:
 
 
 # ---- multi-GPU plumbing (one process per GPU; games shard, no data-path
-# collective). Kept device-agnostic so tests/test_dist_cpu.py runs it with gloo.
+# collective). Device-agnostic, so tests/test_dist_cpu.py runs it with gloo.
 
 def dist_env() -> tuple[int, int, int]:
     """(world, rank, local_rank) from the torchrun environment (1, 0, 0 if unset)."""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def under_launcher() -> bool:
+    return "WORLD_SIZE" in os.environ
 
 
 def shard_seeds(seed: int, rank: int) -> tuple[int, int]:
@@ -155,7 +207,47 @@ def aggregate_rate(world: int, games: int, sims_per_search: int, steps: int, dt_
     return world * games * sims_per_search * steps / dt_max
 
 
-def main() -> None:
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(nproc: int, argv: list[str], port: int) -> list[str]:
+    """The driver's own N>1 launch, for a bare `bench.py --gpus N`."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+
+
+def launch_ranks(args, argv: list[str]) -> int:
+    """Bare `bench.py --gpus N` (N > 1, no launcher in the environment): start
+    the N rank processes as a torch.distributed.run child and return its exit
+    code. Runs before any HIP call of this process (device_count() does not
+    initialise the GPU on this image), and never execs: the child is a new
+    process. Without the gloo rehearsal the GPUs must be there."""
+    backend = os.environ.get("OAMD_BENCH_BACKEND", "nccl")
+    if not args.dry_run and backend != "gloo":
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {have} "
+                  "(OAMD_BENCH_BACKEND=gloo rehearses ranks that share GPUs; its line is labelled a "
+                  "rehearsal)", file=sys.stderr)
+            return 2
+    cmd = launch_command(args.gpus, argv, free_port())
+    print(f"bench.py: starting {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def check_ranks(args, world: int, backend: str, ranks: list[dict]) -> None:
+    """Refuse a line that would misstate the job: ranks != --gpus, or ranks
+    sharing GPUs outside the explicit gloo rehearsal."""
+    n_devices = len({r["device"] for r in ranks})
+    if n_devices < world and backend != "gloo":
+        raise SystemExit(f"bench.py: {world} ranks ran on {n_devices} distinct device(s); every rank needs its "
+                         "own GPU (OAMD_BENCH_BACKEND=gloo rehearses shared GPUs)")
+
+
+def parse_args(argv: list[str]):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -174,128 +266,148 @@ def main() -> None:
                          "configs[4] uses 2048")
     ap.add_argument("--pipeline", type=int, default=0, help="pipeline groups (0 = engine default: 2)")
     ap.add_argument("--nn-chains", type=int, default=1, help="concurrent chains of ResNet launches")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-baseline-moves", type=int, default=24,
+                    help="timed moves of the CPU baseline (0 = skip it), after 2 warm-up moves")
+    ap.add_argument("--cpu-baseline-threads", type=int, default=0,
+                    help="torch threads of the CPU baseline (0 = every CPU this process may use)")
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
     ap.add_argument("--timing-every", type=int, default=5,
                     help="record the kernels' HIP events on every N-th timed search (1 = all; the event "
                          "packets add ~10 us per NN launch boundary to the searches they time)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank plumbing only: no GPU, no search (gloo, each step a fixed sleep)")
+    ap.add_argument("--dry-step-ms", type=float, default=20.0, help="--dry-run: ms per step (rank r: x (1 + r))")
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    return args
 
+
+class DryWorkload:
+    """--dry-run: the bench's rank path with a fixed sleep per step instead of
+    the GPU search (rank r sleeps (1 + r) x dry_step_ms, so the max over ranks
+    is the last rank's)."""
+
+    def __init__(self, args, rank: int, local: int) -> None:
+        self.args = args
+        self.rank = rank
+        self.device_id = f"{socket.gethostname()}:dry{local}"
+
+    def step(self) -> None:
+        time.sleep(self.args.dry_step_ms * 1e-3 * (1 + self.rank))
+
+    def sync(self) -> None:
+        pass
+
+
+def main(argv: list[str] | None = None) -> None:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.gpus > 1 and not under_launcher():
+        raise SystemExit(launch_ranks(args, argv))
     world, rank, local = dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     # OAMD_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
     # devices round-robin, timing reduced over gloo); the driver's runs use RCCL
-    backend = os.environ.get("OAMD_BENCH_BACKEND", "nccl")
+    backend = "gloo" if args.dry_run else os.environ.get("OAMD_BENCH_BACKEND", "nccl")
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        return report(args, world, rank, backend, DryWorkload(args, rank, local))
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
+    elif local >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} (local {local}) has no GPU: "
+                         f"{torch.cuda.device_count()} visible")
     torch.cuda.set_device(local)
     if world > 1:
         if backend == "gloo":
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return report(args, world, rank, backend, EngineWorkload(args, rank, local))
 
-    import othello_mcts as om
-    from othello_mcts.synthetic import alphazero_state_dict
 
-    R = args.blocks - 1
-    sd = alphazero_state_dict(args.seed, 1 + 2 * args.history, args.channels, R, args.hidden)
-    net = om.NativeNet(sd, device=local, dtype=args.dtype)
-    engine_seed, opening_seed = shard_seeds(args.seed, rank)
-    b = om.BatchedMCTS(args.games, history_size=args.history, num_simulations=args.sims,
-                       num_threads=args.threads, batch_size=args.batch, seed=engine_seed)
-    b.random_openings(8, seed=opening_seed)
+class EngineWorkload:
+    """configs[1] on this rank's GPU: `games` self-play games, one step = one
+    search of every game + the on-device self-play move."""
+
+    def __init__(self, args, rank: int, local: int) -> None:
+        import othello_mcts as om
+        from othello_mcts.synthetic import alphazero_state_dict
+
+        self.args = args
+        self.local = local
+        R = args.blocks - 1
+        sd = alphazero_state_dict(args.seed, 1 + 2 * args.history, args.channels, R, args.hidden)
+        self.net = om.NativeNet(sd, device=local, dtype=args.dtype)
+        engine_seed, opening_seed = shard_seeds(args.seed, rank)
+        self.b = om.BatchedMCTS(args.games, history_size=args.history, num_simulations=args.sims,
+                                num_threads=args.threads, batch_size=args.batch, seed=engine_seed)
+        self.b.random_openings(8, seed=opening_seed)
+        if args.eval_batch:  # rows per ResNet launch; the 2 pipeline groups stay
+            self.b.engine.set_nn_batch(args.eval_batch)
+        if args.pipeline:
+            self.b.engine.set_pipeline(args.pipeline)
+        self.b.engine.set_nn_chains(args.nn_chains)
+        props = torch.cuda.get_device_properties(local)
+        self.device_id = f"{os.uname().nodename}:{getattr(props, 'uuid', local)}"
+
+    def step(self) -> None:
+        self.b.search(self.net, sync=self.args.sync_search)  # enqueue only; the timed region syncs at its end
+        self.b.selfplay_move(temperature_moves=12, opening_moves=8, emit_targets=True)
+
+    def sync(self) -> None:
+        torch.cuda.synchronize()
+
+    def start_measuring(self) -> None:
+        e = self.b.engine
+        e.enable_timing(max(1, self.args.timing_every))
+        self.t0 = (e.nn_timing(), e.tree_timing(), e.work_counters())
+
+    def stop_measuring(self) -> dict:
+        e = self.b.engine
+        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0) = self.t0
+        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1) = e.nn_timing(), e.tree_timing(), e.work_counters()
+        overflow_games, depth_capped = e.status()
+        if overflow_games or depth_capped:
+            raise SystemExit(f"bench invalid: {overflow_games} game(s) overflowed their node pool, "
+                             f"{depth_capped} hit the depth cap")
+        return {"nn_ms": ms1 - ms0, "nn_launches": la1 - la0, "nn_rows": rw1 - rw0, "select_ms": se1 - se0,
+                "backup_ms": bk1 - bk0, "tree_launches": tl1 - tl0, "sims": si1 - si0, "evals": ev1 - ev0,
+                "overflow_games": overflow_games}
+
+
+def report(args, world: int, rank: int, backend: str, wl) -> None:
     L = args.threads * args.batch
-    if args.eval_batch:  # rows per ResNet launch; the 2 pipeline groups stay
-        b.engine.set_nn_batch(args.eval_batch)
-    if args.pipeline:
-        b.engine.set_pipeline(args.pipeline)
-    b.engine.set_nn_chains(args.nn_chains)
     sims_per_search = L * ((args.sims + L - 1) // L)
-
-    def step():
-        b.search(net, sync=args.sync_search)  # enqueue only; the timed region syncs at its end
-        b.selfplay_move(temperature_moves=12, opening_moves=8, emit_targets=True)
-
     for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    b.engine.enable_timing(max(1, args.timing_every))
-    ms0, launches0, rows0 = b.engine.nn_timing()
-    sel0, bk0, tree_launches0 = b.engine.tree_timing()
+        wl.step()
+    wl.sync()
+    measuring = hasattr(wl, "start_measuring")
+    if measuring:
+        wl.start_measuring()
 
     def run():
         for _ in range(args.steps):
-            step()
+            wl.step()
 
-    dt_max = timed_max(world, run, torch.cuda.synchronize, "cpu" if backend == "gloo" else "cuda")
-    ms1, launches1, rows1 = b.engine.nn_timing()
-    sel1, bk1, tree_launches1 = b.engine.tree_timing()
+    dt_max = timed_max(world, run, wl.sync, "cuda" if backend == "nccl" else "cpu")
+    m = wl.stop_measuring() if measuring else None
     value = aggregate_rate(world, args.games, sims_per_search, args.steps, dt_max)
-    # every game's search followed the reference: no node pool ran out
-    overflow_games, depth_capped = b.engine.status()
-    if overflow_games or depth_capped:
-        raise SystemExit(f"bench invalid: {overflow_games} game(s) overflowed their node pool, "
-                         f"{depth_capped} hit the depth cap")
-    props = torch.cuda.get_device_properties(local)
-    dev_id = f"{os.uname().nodename}:{getattr(props, 'uuid', local)}"
-    ranks = rank_table(world, rank, dev_id, args.games * sims_per_search * args.steps)
+    ranks = rank_table(world, rank, wl.device_id, args.games * sims_per_search * args.steps)
+    check_ranks(args, world, backend, ranks)
     n_devices = len({r["device"] for r in ranks})
-
-    nn_ms = ms1 - ms0
-    nn_launches = launches1 - launches0
-    nn_rows = rows1 - rows0
-    flops = resnet_flops_per_eval(1 + 2 * args.history, args.channels, R, args.hidden)
-    avg_ms = nn_ms / max(1, nn_launches)
-    rows_per_launch = nn_rows / max(1, nn_launches)
-    achieved = flops * rows_per_launch / (avg_ms * 1e-3) / 1e12
-    executed = flops - 2.0 * 64 * 9 * args.channels * args.channels * 2 * R // 12
-    peak = PEAK_TFLOPS[args.dtype]
     workload = (f"{args.games} concurrent self-play games per GPU, {args.sims} sims/move, "
                 f"{args.channels}x{args.blocks}b ResNet {args.dtype}, history {args.history}, "
                 f"{args.threads} threads x {args.batch} leaves per step"
                 + (f", eval batch {args.eval_batch}" if args.eval_batch else "")
                 + (" (BASELINE configs[1])" if (args.games, args.channels, args.blocks, args.sims, args.dtype,
                                                 args.eval_batch) == (256, 128, 10, 800, "bf16", 0) else ""))
-    # HBM bytes per launch from the committed PMC summary of this same workload
-    traffic = None
-    tfile = ROOT / "profiles" / "traffic_resnet.json"
-    if tfile.exists():
-        try:
-            tj = json.loads(tfile.read_text())
-            if tj.get("workload") == workload and tj.get("rows_per_launch") == int(rows_per_launch):
-                traffic = tj.get("bytes_per_launch")
-        except (ValueError, OSError):
-            traffic = None
-
-    # tree kernels: latency-bound (one wave per game, dependent loads); HBM bytes
-    # per launch from the committed PMC summary of this workload, if present
-    tree_bytes = {}
-    tfile = ROOT / "profiles" / "traffic_tree.json"
-    if tfile.exists():
-        try:
-            tj = json.loads(tfile.read_text())
-            if tj.get("workload") == workload and tj.get("rows_per_launch") == int(rows_per_launch):
-                tree_bytes = {k: v["bytes_per_launch"] for k, v in tj["kernels"].items()}
-        except (ValueError, OSError, KeyError):
-            tree_bytes = {}
-    # k_tree: one launch per search round and pipeline group; "select" rounds
-    # back up the previous batch and select the next, the final round backs up
-    tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch)}
-    tree_launches = tree_launches1 - tree_launches0  # select rounds x pipeline groups
-    steps_per_search = (args.sims + L - 1) // L
-    for name, ms, n in (("k_tree", sel1 - sel0, tree_launches),
-                        ("k_tree_final_backup", bk1 - bk0, tree_launches // steps_per_search)):
-        avg = ms / max(1, n)
-        entry = {"avg_launch_ms": round(avg, 4)}
-        if name in tree_bytes:
-            gbs = tree_bytes[name] / (avg * 1e-3) / 1e9
-            entry.update({"hbm_bytes_per_launch": tree_bytes[name], "achieved_GB_s": round(gbs, 2),
-                          "frac_hbm_peak": round(gbs / PEAK_HBM_GBS, 5)})
-        tree[name] = entry
-
     result = {
-        "metric": "MCTS simulations/sec (whole node), 800 sims/move, 128x10b ResNet, 1/2/4/8 GPU",
+        "metric": METRIC,
         "value": round(value, 1),
         "unit": "simulations/s",
         "n_gpus": n_devices,
@@ -308,8 +420,9 @@ def main() -> None:
         "baseline_ref": {"value": PUBLISHED_SIMS_PER_S, "unit": "simulations/s",
                          "hardware": "1x RTX 4090 + 24-core CPU (reference README.md:25, BASELINE.md)"},
         "dtype": args.dtype,
-        "data": f"synthetic: seeded random-init {args.channels}x{args.blocks}b AlphaZeroNet weights, "
-                "random openings (0-8 plies)",
+        "data": (f"synthetic: seeded random-init {args.channels}x{args.blocks}b AlphaZeroNet weights, "
+                 "random openings (0-8 plies)") if m is not None else
+                "DRY RUN: rank plumbing only, no GPU work (each step a fixed sleep); not a measurement",
         "config": {
             "workload": workload,
             "games_per_gpu": args.games,
@@ -321,7 +434,75 @@ def main() -> None:
             "ranks": ranks,
             "backend": (backend if world > 1 else "none"),
         },
-        "overflow_games": overflow_games,
+    }
+    if args.dry_run:
+        result["dry_run"] = True
+    if m is not None:
+        result.update(measured_fields(args, m, workload))
+        if rank == 0 and world == 1 and args.cpu_baseline_moves > 0:
+            result["cpu_baseline"] = cpu_baseline(args.history, args.channels, args.blocks - 1, args.hidden,
+                                                  moves=args.cpu_baseline_moves,
+                                                  threads=args.cpu_baseline_threads or None)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def measured_fields(args, m: dict, workload: str) -> dict:
+    """roofline (the fused ResNet kernel), tree-kernel timings and the work
+    counters of this rank's timed region."""
+    R = args.blocks - 1
+    flops = resnet_flops_per_eval(1 + 2 * args.history, args.channels, R, args.hidden)
+    avg_ms = m["nn_ms"] / max(1, m["nn_launches"])
+    rows_per_launch = m["nn_rows"] / max(1, m["nn_launches"])
+    # n_eval: rows of non-terminal leaves (BASELINE.md: the MFMA fraction is
+    # over evaluated simulations); terminal rows are launched but their
+    # workgroups stop at the prologue when a whole workgroup is terminal
+    rows_launched = args.games * args.threads * args.batch * ((args.sims + args.threads * args.batch - 1)
+                                                              // (args.threads * args.batch)) * args.steps
+    eval_share = m["evals"] / max(1, rows_launched)
+    n_eval_per_launch = rows_per_launch * eval_share
+    achieved = flops * n_eval_per_launch / (avg_ms * 1e-3) / 1e12
+    achieved_launched = flops * rows_per_launch / (avg_ms * 1e-3) / 1e12
+    executed = flops - 2.0 * 64 * 9 * args.channels * args.channels * 2 * R // 12
+    peak = PEAK_TFLOPS[args.dtype]
+    # HBM bytes per launch from the committed PMC summary of this same workload
+    traffic = None
+    tfile = ROOT / "profiles" / "traffic_resnet.json"
+    if tfile.exists():
+        try:
+            tj = json.loads(tfile.read_text())
+            if tj.get("workload") == workload and tj.get("rows_per_launch") == int(rows_per_launch):
+                traffic = tj.get("bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+    tree_bytes = {}
+    tfile = ROOT / "profiles" / "traffic_tree.json"
+    if tfile.exists():
+        try:
+            tj = json.loads(tfile.read_text())
+            if tj.get("workload") == workload and tj.get("rows_per_launch") == int(rows_per_launch):
+                tree_bytes = {k: v["bytes_per_launch"] for k, v in tj["kernels"].items()}
+        except (ValueError, OSError, KeyError):
+            tree_bytes = {}
+    # k_tree: one launch per search round and pipeline group; "select" rounds
+    # back up the previous batch and select the next, the final round backs up
+    tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch)}
+    steps_per_search = (args.sims + args.threads * args.batch - 1) // (args.threads * args.batch)
+    for name, ms, n in (("k_tree", m["select_ms"], m["tree_launches"]),
+                        ("k_tree_final_backup", m["backup_ms"], m["tree_launches"] // steps_per_search)):
+        avg = ms / max(1, n)
+        entry = {"avg_launch_ms": round(avg, 4)}
+        if name in tree_bytes:
+            gbs = tree_bytes[name] / (avg * 1e-3) / 1e9
+            entry.update({"hbm_bytes_per_launch": tree_bytes[name], "achieved_GB_s": round(gbs, 2),
+                          "frac_hbm_peak": round(gbs / PEAK_HBM_GBS, 5)})
+        tree[name] = entry
+    return {
+        "overflow_games": m["overflow_games"],
+        "work": {"simulations": m["sims"], "n_eval": m["evals"], "rows_launched": rows_launched,
+                 "terminal_share": round(1.0 - eval_share, 5)},
         "roofline": {
             "bound": "mfma",
             "kernel": "k_resnet_w8 (fused 19-conv tower + heads, 8-wave geometry)",
@@ -330,24 +511,22 @@ def main() -> None:
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
+            "basis": "n_eval rows (non-terminal leaves) per launch x flops_per_row / mean launch time",
             "avg_launch_ms": round(avg_ms, 4),
             "rows_per_launch": int(rows_per_launch),
+            "n_eval_per_launch": round(n_eval_per_launch, 1),
             "flops_per_row": flops,
+            # every launched row counted as work (the round-2 basis)
+            "achieved_rows_launched": round(achieved_launched, 2),
+            "frac_rows_launched": round(achieved_launched / peak, 4),
             # the default build leaves out the tower MFMAs whose activations are
             # all zero border (1/12 of every tower conv): achieved
             # counts the algorithmic FLOPs above, these are the ones executed
             "executed_flops_per_row": executed,
-            "executed_TFLOP_s": round(executed * rows_per_launch / (avg_ms * 1e-3) / 1e12, 2),
+            "executed_TFLOP_s": round(executed * n_eval_per_launch / (avg_ms * 1e-3) / 1e12, 2),
         },
         "tree_kernels": tree,
     }
-    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.history, args.channels, R,
-                                              args.hidden)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -157,6 +157,12 @@ int oamd_engine_reset(oamd_engine *e, int32_t game, uint64_t seed);
  * rows on a stream of their own while the next thread's tree work runs
  * (same results; OAMD_TREE_SPLIT=0 in the environment turns it off). */
 int oamd_engine_search(oamd_engine *e, oamd_net *net, int64_t *simulations, int64_t *evaluations);
+/* Work done since the engine was created (host outputs; waits for the
+ * engine's stream): simulations (leaf selections) and evaluations (NN rows of
+ * non-terminal leaves, BASELINE.md's n_eval) over every search, native or
+ * step-wise. The reference counts neither; it builds no NN row for a terminal
+ * leaf (search_thread.cpp:88-90). */
+int oamd_engine_work_counters(oamd_engine *e, int64_t *simulations, int64_t *evaluations);
 /* Split the games into `groups` pipeline groups (own HIP streams) so that tree
  * kernels of one group overlap the NN launch of another (0 = auto: 2 groups
  * from 64 games, else 1; at most 8). Results do not depend on it. */
@@ -257,10 +263,9 @@ int oamd_engine_game_key(oamd_engine *e, int32_t game, uint64_t *key_host);
 
 /* Timing accumulated over the timed oamd_engine_search calls (HIP events on
  * the launching streams; a query waits for the searches still in flight):
- * total ms spent in the NN kernel, number of NN launches, rows evaluated.
- * With two pipeline groups on prioritised streams (opt-in, OAMD_NN_PRIO=1)
- * only group 0's launches are counted: group 1's launch is enqueued before it
- * can dispatch, so its events would include the wait behind group 0's. */
+ * total ms spent in the NN kernel, number of NN launches, rows launched
+ * (terminal leaves included; oamd_engine_work_counters gives the rows that
+ * needed an evaluation). */
 int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches, int64_t *rows);
 /* Same for the tree kernel (k_tree, one launch per search round and pipeline
  * group): select_ms = total ms of the rounds that select (each also backs up

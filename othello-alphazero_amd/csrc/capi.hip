@@ -162,6 +162,7 @@ struct oamd_engine {
     // rows are evaluated by consecutive launches on its stream
     int nn_batch = 0;
     int n_pipe_streams = 0;
+    int n_events = 0;  // sel_ev / nn_ev pairs created
     hipStream_t pipe_stream[kMaxPipeline] = {};
     hipEvent_t fork_ev = nullptr;
     // NN tokens: the pipeline groups' ResNet launches form nn_chains chains
@@ -225,15 +226,6 @@ struct oamd_engine {
     }
 
     int L() const { return cfg.num_threads * cfg.batch_size; }
-    // Opt-in (OAMD_NN_PRIO=1 in the environment): two pipeline groups on
-    // prioritised streams (group 0 high, group 1 low); group 1's ResNet launch
-    // no longer waits for group 0's to complete, group 0 still waits for group
-    // 1's previous launch (two priority levels cannot order a cycle). Bench C2,
-    // same box: 4.31 vs 4.27 M sims/s (tools/prio_ab.sh), but the priority does
-    // not hold the dispatch order: the two groups' launches share the CUs for
-    // most of their run (kernel trace: 1.16 / 1.54 ms per launch instead of
-    // 0.91), so a launch's duration no longer measures the kernel. Off by
-    // default, so the bench's roofline stays a per-launch measurement.
     // thread-split schedule for one game (OAMD_TREE_SPLIT=0 in the environment: off)
     static bool tree_split() {
         static const bool v = [] {
@@ -242,33 +234,25 @@ struct oamd_engine {
         }();
         return v;
     }
-    static bool nn_prio() {
-        static const bool v = [] {
-            const char* e = getenv("OAMD_NN_PRIO");
-            return e ? atoi(e) != 0 : false;
-        }();
-        return v;
-    }
-
-    int ensure_streams(int K) {
-        if (K <= 1) return OAMD_OK;
+    // K group streams (2 in the single-game thread split) and their events; the
+    // thread split needs a select / NN event pair per virtual thread (nev >= K)
+    int ensure_streams(int K, int nev) {
+        if (K <= 1 && nev <= 1) return OAMD_OK;
         if (!fork_ev) HIPCHK(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
         for (int c = 0; c < kMaxChains; ++c)
             if (!nn_token[c]) HIPCHK(hipEventCreateWithFlags(&nn_token[c], hipEventDisableTiming));
         if (!nn_stream) HIPCHK(hipStreamCreateWithFlags(&nn_stream, hipStreamNonBlocking));
         while (n_pipe_streams < K) {
             const int k = n_pipe_streams;
-            if (nn_prio() && K == 2) {
-                int least = 0, greatest = 0;
-                HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-                HIPCHK(hipStreamCreateWithPriority(&pipe_stream[k], hipStreamNonBlocking, k == 0 ? greatest : least));
-            } else {
-                HIPCHK(hipStreamCreateWithFlags(&pipe_stream[k], hipStreamNonBlocking));
-            }
+            HIPCHK(hipStreamCreateWithFlags(&pipe_stream[k], hipStreamNonBlocking));
             HIPCHK(hipEventCreateWithFlags(&join_ev[k], hipEventDisableTiming));
+            ++n_pipe_streams;
+        }
+        while (n_events < nev) {
+            const int k = n_events;
             HIPCHK(hipEventCreateWithFlags(&sel_ev[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&nn_ev[k], hipEventDisableTiming));
-            ++n_pipe_streams;
+            ++n_events;
         }
         return OAMD_OK;
     }
@@ -361,6 +345,8 @@ struct oamd_engine {
         for (int k = 0; k < n_pipe_streams; ++k) {
             (void)hipStreamDestroy(pipe_stream[k]);
             (void)hipEventDestroy(join_ev[k]);
+        }
+        for (int k = 0; k < n_events; ++k) {
             (void)hipEventDestroy(sel_ev[k]);
             (void)hipEventDestroy(nn_ev[k]);
         }
@@ -671,6 +657,10 @@ int oamd_net_load_state(oamd_net* net, const float* const* t, int32_t n_tensors)
                 hconv[((size_t)cb * 64 + lane) * 8 + j] = d.dtype == OAMD_BF16 ? f32_to_bf16_rne(v) : f32_to_f16(v);
             }
     DeviceGuard dg(net->device);
+    // searches run the ResNet on non-blocking streams, which a plain hipMemcpy
+    // does not order against: let every launch still reading these buffers
+    // finish before they are overwritten (a weight refresh between searches)
+    HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(net->hconv, hconv.data(), hconv.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(net->w, packed.data(), packed.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(net->bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
@@ -713,13 +703,17 @@ int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity,
     e->seed = seed;
     const size_t nodes = (size_t)num_games * node_capacity;
     if ((rc = dalloc(&e->link, nodes)) || (rc = dalloc(&e->stat, nodes)) || (rc = dalloc(&e->pos, nodes)) ||
-        (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) || (rc = dalloc(&e->counters, 2)) ||
+        (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) || (rc = dalloc(&e->counters, 4)) ||
         (rc = dalloc(&e->status_dev, 2)) || (rc = dalloc(&e->info_dev, num_games)) || (rc = dalloc(&e->visits_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->q_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->spd_dev, (size_t)8 * (1 + 2 * kMaxHistory) * 64 + 8 * 65)) || (rc = e->alloc_rows()) ||
         (rc = e->build_tables())) {
         delete e;
         return rc;
+    }
+    if (hipMemset(e->counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        delete e;
+        return fail(OAMD_RUNTIME, "engine init: counter memset failed");
     }
     launch_reset(e->view(), -1, seed, nullptr);
     hipError_t le = hipGetLastError();
@@ -886,7 +880,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     // as in one launch per round, so results are identical.
     const bool split = e->G == 1 && K == 1 && T > 1 && T <= kMaxPipeline && e->tree_split();
     const int NB = split ? T : K;  // timing blocks per round
-    int rc = e->ensure_streams(split ? T : K);
+    int rc = split ? e->ensure_streams(2, T) : e->ensure_streams(K, K);
     if (rc) return rc;
     if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
     // sampled timing: every timing_stride-th search records its events
@@ -916,7 +910,6 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     // rounds 0..steps (k_tree): round s backs up batch s-1 and selects batch s,
     // thread by thread; the NN evaluates batch s between rounds s and s+1
     const int nch = e->nn_chains < K ? e->nn_chains : K;
-    const bool prio = K == 2 && e->nn_prio() && OAMD_NN_ORDER == 1;
     for (int s = 0; split && s <= steps; ++s) {
         for (int t = 0; t < T; ++t) {
             hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * T + t)] : nullptr;
@@ -949,14 +942,10 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
                 ns = e->nn_stream;
                 HIPCHK(hipEventRecord(e->sel_ev[k], st[k]));
                 HIPCHK(hipStreamWaitEvent(ns, e->sel_ev[k], 0));
-            } else if (prio) {
-                if (k == 0 && s > 0) HIPCHK(hipStreamWaitEvent(st[k], e->nn_token[0], 0));
             } else if (K > 1 && OAMD_NN_ORDER == 1 && (s > 0 || k >= nch)) {
                 HIPCHK(hipStreamWaitEvent(st[k], e->nn_token[k % nch], 0));
             }
-            // prioritised groups: group 1's launch waits for dispatch behind group 0's,
-            // so only group 0's events bracket a kernel's own run time
-            const bool nn_timed = ev && !(prio && k > 0);
+            const bool nn_timed = ev != nullptr;
             if (nn_timed) HIPCHK(hipEventRecord(ev[2], ns));
             const int grows = ng[k] * L;
             const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
@@ -967,8 +956,6 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             if (K > 1 && OAMD_NN_ORDER == 2) {
                 HIPCHK(hipEventRecord(e->nn_ev[k], ns));
                 HIPCHK(hipStreamWaitEvent(st[k], e->nn_ev[k], 0));
-            } else if (prio) {
-                if (k == 1) HIPCHK(hipEventRecord(e->nn_token[0], st[k]));
             } else if (K > 1 && OAMD_NN_ORDER == 1) {
                 HIPCHK(hipEventRecord(e->nn_token[k % nch], st[k]));
             }
@@ -985,7 +972,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
         e->ev_blocks[pool] = (steps + 1) * NB;
         e->ev_final[pool] = steps * NB;
         e->ev_K[pool] = NB;
-        e->ev_nn_groups[pool] = prio ? 1 : NB;
+        e->ev_nn_groups[pool] = NB;
         int64_t nl = 0, rows = 0;
         if (split) {
             nl = T;
@@ -1010,6 +997,16 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     }
     e->step_phase = 0;
     e->steps_left = 0;
+    return OAMD_OK;
+}
+
+int oamd_engine_work_counters(oamd_engine* e, int64_t* sims, int64_t* evals) {
+    DeviceGuard dg(e->device);
+    unsigned long long c[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(c, e->counters + 2, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (sims) *sims = (int64_t)c[0];
+    if (evals) *evals = (int64_t)c[1];
     return OAMD_OK;
 }
 

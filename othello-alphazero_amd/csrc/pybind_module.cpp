@@ -663,6 +663,11 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
             check(oamd_engine_nn_timing(e.h, &ms, &launches, &rows));
             return py::make_tuple(ms, launches, rows);
         })
+        .def("work_counters", [](Engine& e) {
+            int64_t sims = 0, evals = 0;
+            check(oamd_engine_work_counters(e.h, &sims, &evals));
+            return py::make_tuple(sims, evals);
+        })
         .def("tree_timing", [](Engine& e) {
             float sel, bk;
             int64_t launches;

@@ -965,6 +965,24 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     int slot = 0;  // g % RING
 
     OAMD_STAMP(7);
+    if constexpr (IN == kPacked) {
+        // Terminal leaves need no evaluation: the reference builds no NN row
+        // for them and skips a thread's NN call when its whole batch is
+        // terminal (search_thread.cpp:83-111); their policy / value rows are
+        // never read (backup_range scores them from the discs). A workgroup
+        // whose boards are all terminal (or past the end) therefore stops
+        // here, once its weight DMAs have landed (the LDS they write is
+        // released with the workgroup). Scalar loads of uniform addresses.
+        bool live = false;
+#pragma unroll
+        for (int b = 0; b < G::BOARDS; ++b)
+            if (row0 + b < rows)
+                live |= ((reinterpret_cast<const uint64_t*>(feat_in)[(size_t)(row0 + b) * fw] >> 16) & 1ULL) != 0;
+        if (!live) {
+            wait_vm<0>();
+            return;
+        }
+    }
     // stage 0 and the input planes must be visible (bias loads are older than the DMAs)
     if constexpr (G::EARLY) wait_vm<G::DPT>();  // stage 0 landed (over-waits for stage 1: once)
     else if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();

@@ -479,10 +479,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     if (lane == 0) {
         gs->event = event;
         gs->count = count;
-        if (overflow) gs->flags |= kOverflow;
+        // atomic like select_range's kDepthCap: a plain read-modify-write of
+        // the flags read at kernel start could drop that bit
+        if (overflow) atomicOr(&gs->flags, (int)kOverflow);
         if (E.counters && do_select) {
+            // [0..1] this search (reset when a caller asks for them), [2..3]
+            // cumulative since the engine was created (oamd_engine_work_counters)
             atomicAdd(E.counters + 0, sims);
             atomicAdd(E.counters + 1, evals);
+            atomicAdd(E.counters + 2, sims);
+            atomicAdd(E.counters + 3, evals);
         }
     }
 }

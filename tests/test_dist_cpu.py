@@ -1,6 +1,10 @@
 """Multi-process path of bench.py (section 5 of the task: games shard, no
-data-path collective) on CPU with gloo, world_size 2, launched exactly like the
-driver's N>1 run: python -m torch.distributed.run --master-addr 127.0.0.1."""
+data-path collective) on the CPU: the real bench.main() rank path in --dry-run
+mode (gloo, no GPU, each step a fixed sleep), launched both ways the driver
+may start it — bare `bench.py --gpus 2`, which starts its own
+torch.distributed.run child, and the driver's own `python -m
+torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 bench.py
+--gpus 2` — and the refusals: ranks != --gpus, and --gpus N without N GPUs."""
 
 import json
 import os
@@ -10,6 +14,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
+BENCH = str(ROOT / "bench.py")
 
 
 def _free_port() -> int:
@@ -18,30 +23,72 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def test_two_rank_gloo_bench_plumbing():
+def _env() -> dict:
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "dist_worker.py")]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    env.pop("WORLD_SIZE", None)
+    env.pop("OAMD_BENCH_BACKEND", None)
+    return env
+
+
+def _run(cmd, timeout=300):
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=_env(), cwd=ROOT)
+
+
+def _one_line(r) -> dict:
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 prints exactly one line
-    out = json.loads(lines[0])
-    assert out["world"] == 2
-    shards = sorted(out["shards"], key=lambda s: s["rank"])
-    assert [s["rank"] for s in shards] == [0, 1] and [s["local"] for s in shards] == [0, 1]
-    # every rank saw the same max-over-ranks time, at least the slow rank's sleep
-    assert shards[0]["dt_max"] == shards[1]["dt_max"] == out["dt_max"] >= 0.2
-    # whole-job rate = all ranks' units / max time
-    assert abs(out["rate"] - 2 * 2 * 32 / out["dt_max"]) < 1e-6 * out["rate"]
-    # disjoint shards: distinct RNG keys and openings per rank, so different searches
-    assert shards[0]["seeds"] != shards[1]["seeds"]
-    assert shards[0]["played"] != shards[1]["played"]
-    assert all(0 < sum(v) <= 32 for s in shards for v in s["played"])
-    # the rank table names every rank's device and units (bench.py's n_gpus =
-    # distinct devices, so ranks sharing a GPU are not counted twice)
-    assert [r["rank"] for r in out["ranks"]] == [0, 1]
-    assert len({r["device"] for r in out["ranks"]}) == 2 and all(r["sims"] == 64 for r in out["ranks"])
+    return json.loads(lines[0])
+
+
+def _check_two_rank_line(out: dict, steps: int, step_ms: float, games: int) -> None:
+    assert out["dry_run"] is True and "DRY RUN" in out["data"]
+    assert out["metric"].startswith("MCTS simulations/sec (whole node)")
+    assert out["n_gpus"] == 2 and out["steps"] == steps and out["scaling"] == "weak"
+    ranks = sorted(out["config"]["ranks"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert len({r["device"] for r in ranks}) == 2
+    assert all(r["sims"] == games * 800 * steps for r in ranks)
+    # the max over ranks: rank 1 sleeps 2 x step_ms per step
+    dt = out["ms_per_step"] * steps / 1e3
+    assert dt >= steps * 2 * step_ms / 1e3
+    # whole-job rate = both ranks' units / the max time
+    assert abs(out["value"] - 2 * games * 800 * steps / dt) <= 1e-3 * out["value"] + 0.1
+    assert "REHEARSAL" not in out["config"]["parallelism"] and out["config"]["backend"] == "gloo"
+    assert "roofline" not in out and "cpu_baseline" not in out
+
+
+def test_bare_bench_gpus2_starts_its_own_ranks():
+    r = _run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1",
+              "--games", "4", "--dry-step-ms", "30"])
+    assert "starting 2 ranks" in r.stderr
+    _check_two_rank_line(_one_line(r), 3, 30.0, 4)
+
+
+def test_driver_launch_gpus2():
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+              "--master-addr=127.0.0.1", f"--master-port={_free_port()}", BENCH,
+              "--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "0", "--games", "8", "--dry-step-ms", "25"])
+    assert "starting" not in r.stderr  # under a launcher bench.py starts nothing itself
+    _check_two_rank_line(_one_line(r), 2, 25.0, 8)
+
+
+def test_ranks_must_match_gpus():
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+              "--master-addr=127.0.0.1", f"--master-port={_free_port()}", BENCH,
+              "--gpus", "1", "--dry-run", "--steps", "1", "--warmup", "0"])
+    assert r.returncode != 0
+    assert "--gpus 1 but the launcher started 2 rank(s)" in r.stdout + r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_gpus_without_gpus_fails_loudly():
+    # this container has no GPU: a real (non-dry, non-rehearsal) 2-GPU run must
+    # refuse before starting anything
+    r = _run([sys.executable, BENCH, "--gpus", "2", "--steps", "1"], timeout=120)
+    assert r.returncode != 0
+    assert "needs 2 visible GPUs, found 0" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
 
 
 def test_single_rank_helpers():
@@ -53,3 +100,17 @@ def test_single_rank_helpers():
     calls = []
     dt = bench.timed_max(1, lambda: calls.append(1), lambda: calls.append(0), "cpu")
     assert calls == [0, 1, 0] and dt >= 0.0
+    cpus = bench.usable_cpus()
+    assert 1 <= cpus["usable"] <= cpus["nproc"]
+    cmd = bench.launch_command(4, ["--gpus", "4"], 1234)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and cmd[-2:] == ["--gpus", "4"]
+    # ranks sharing a device are refused outside the gloo rehearsal
+    import pytest
+
+    class A:
+        gpus = 2
+    shared = [{"rank": 0, "device": "h:u0", "sims": 1}, {"rank": 1, "device": "h:u0", "sims": 1}]
+    with pytest.raises(SystemExit):
+        bench.check_ranks(A, 2, "nccl", shared)
+    bench.check_ranks(A, 2, "gloo", shared)  # the labelled rehearsal

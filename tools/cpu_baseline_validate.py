@@ -11,7 +11,7 @@ SURVEY.md §8(d): 1,705 / 1,295 / 491 sims/s at 8 / 4 / 1 cores, measured when
 the survey was written).
 
 Usage: python tools/cpu_baseline_validate.py [--moves 12]
-Writes profiles/r02_cpu_baseline_validation.json.
+Writes profiles/r03_cpu_baseline_validation.json.
 """
 
 from __future__ import annotations
@@ -75,8 +75,8 @@ def port_leg(threads: int, moves: int) -> dict:
     code = (
         "import sys, json, torch; sys.path.insert(0, %r); sys.path.insert(0, %r); "
         "torch.set_num_threads(%d); import bench; "
-        "r = bench.cpu_baseline(1e9, 8, 128, 9, 128, max_moves=%d, warmup_moves=1); print(json.dumps(r))"
-    ) % (str(ROOT), str(ROOT / "othello-alphazero_amd"), threads, moves)
+        "r = bench.cpu_baseline(8, 128, 9, 128, moves=%d, warmup_moves=1, threads=%d); print(json.dumps(r))"
+    ) % (str(ROOT), str(ROOT / "othello-alphazero_amd"), threads, moves, threads)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True,
                          env={"OMP_NUM_THREADS": str(threads), "PATH": "/usr/bin:/bin"})
     r = json.loads(out.stdout.strip().splitlines()[-1])
@@ -102,7 +102,7 @@ def main() -> None:
     out = {"what": "bench.py cpu_baseline (oracle port) vs the compiled reference, configs[0], same container",
            "cpu_model": bench.cpu_model(), "nproc": __import__("os").cpu_count(),
            "when": time.strftime("%Y-%m-%d %H:%M:%S"), "rows": rows}
-    (ROOT / "profiles" / "r02_cpu_baseline_validation.json").write_text(json.dumps(out, indent=1))
+    (ROOT / "profiles" / "r03_cpu_baseline_validation.json").write_text(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,86 @@
+#!/bin/bash
+# The GPU-box harness: every measurement of DESIGN.md comes from one of these
+# recipes (it replaces round 1/2's one-off A/B scripts). Usage:
+#   bash tools/gpu.sh "RECIPE ARGS..." ["RECIPE ARGS..." ...]
+# Recipes (NAME names the output under $OUT, default gpurun_out/run):
+#   tests [pytest args]            the -m gpu suite                  -> tests.log
+#   smoke                          __graft_entry__.smoke()           -> smoke.log
+#   bench NAME [bench.py args]     one bench line                    -> bench_NAME.json
+#   trace NAME [bench.py args]     rocprofv3 --kernel-trace --stats  -> trace_NAME/
+#   pmc NAME C1,C2,.. [bench args] one rocprofv3 --pmc pass (+ kernel trace) over bench.py -> pmc_NAME/
+#   nn NAME [VAR=val ...]          standalone k_resnet timing (tools/nn_kernel.py; ROWS, NN_C, NN_DTYPE)
+#   nnpmc NAME C1,C2,.. [VAR=val]  one --pmc pass over tools/nn_kernel.py  -> nnpmc_NAME/
+#   latency NAME                   single-game latency (tools/latency.py)
+#   variants NAME [VAR=val ...]    nn timing of every prebuilt abv/<v>/liboamd.so (tools/variants.sh
+#                                  builds them here), ROUNDS interleaved sweeps, outputs compared bit
+#                                  for bit with the first variant's
+#   benchvar NAME [bench args]     bench line of every prebuilt variant, ROUNDS interleaved sweeps
+# Every step runs under its own time limit; the first failing step ends the run
+# (no retries). Summaries: python tools/prof_summary.py (in the build container).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=${OUT:-gpurun_out/run}
+mkdir -p "$OUT"
+PKG=othello-alphazero_amd/othello_mcts
+
+step() {  # step LIMIT LOG cmd...
+  local lim=$1 log=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "== [$rc] $*"
+  tail -2 "$log" | cut -c1-400
+  return $rc
+}
+
+with_vars() {  # with_vars "A=1 B=2" cmd...: env assignments then the command
+  local vars=$1; shift
+  env $vars "$@"
+}
+
+restore_lib() { [ -f /tmp/liboamd.so.orig ] && cp /tmp/liboamd.so.orig $PKG/liboamd.so; }
+
+run_recipe() {
+  local recipe=$1; shift
+  case "$recipe" in
+    tests) step 600 "$OUT/tests.log" python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "$@" ;;
+    smoke) step 300 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) local n=$1; shift; step 900 "$OUT/bench_$n.json" python bench.py "$@" ;;
+    trace) local n=$1; shift
+      step 600 "$OUT/trace_$n.log" rocprofv3 --kernel-trace --stats -T -d "$OUT/trace_$n" -o run \
+        --output-format csv -- python3 bench.py "$@" ;;
+    pmc) local n=$1 c=$2; shift 2
+      step 300 "$OUT/pmc_$n.log" rocprofv3 --pmc ${c//,/ } --kernel-trace -T -d "$OUT/pmc_$n" -o run \
+        --output-format csv -- python3 bench.py "$@" ;;
+    nn) local n=$1; shift; step 300 "$OUT/nn_$n.log" with_vars "$*" python tools/nn_kernel.py ;;
+    nnpmc) local n=$1 c=$2; shift 2
+      step 300 "$OUT/nnpmc_$n.log" with_vars "$*" rocprofv3 --pmc ${c//,/ } --kernel-trace -d "$OUT/nnpmc_$n" \
+        -o run --output-format csv -- python3 tools/nn_kernel.py ;;
+    latency) step 600 "$OUT/latency_$1.log" python tools/latency.py ;;
+    variants) local n=$1; shift
+      cp $PKG/liboamd.so /tmp/liboamd.so.orig
+      local ref=/tmp/ab_ref_$n.pt; rm -f $ref
+      for r in $(seq ${ROUNDS:-2}); do
+        for v in ${AB_ORDER:-$(ls abv)}; do
+          cp abv/$v/liboamd.so $PKG/liboamd.so
+          step 300 "$OUT/var_${n}_${v}_$r.log" with_vars "AB_REF=$ref $*" python tools/nn_kernel.py || { restore_lib; return 1; }
+        done
+      done
+      restore_lib ;;
+    benchvar) local n=$1; shift
+      cp $PKG/liboamd.so /tmp/liboamd.so.orig
+      for r in $(seq ${ROUNDS:-2}); do
+        for v in ${AB_ORDER:-$(ls abv)}; do
+          cp abv/$v/liboamd.so $PKG/liboamd.so
+          step 600 "$OUT/benchvar_${n}_${v}_$r.json" python bench.py --cpu-baseline-moves 0 "$@" || { restore_lib; return 1; }
+        done
+      done
+      restore_lib ;;
+    *) echo "unknown recipe: $recipe"; return 2 ;;
+  esac
+}
+
+for s in "$@"; do
+  # shellcheck disable=SC2086
+  run_recipe $s || exit $?
+done

@@ -1,7 +1,12 @@
-"""Diagnostic: time the fused ResNet kernel (or an ablation variant selected by
-OAMD_RESNET_ABLATE, extension built with OAMD_EXTRA_FLAGS=-DOAMD_ABLATION).
-Ablation variants produce wrong outputs; only their timings matter.
-Prints one line: variant, ms per launch (median of 5 x 10 launches), TFLOP/s."""
+"""Standalone timing of the fused ResNet kernel (csrc/resnet.hip) through
+NativeNet's fp32-input forward, for A/Bs of kernel variants and PMC passes
+(tools/gpu.sh recipes nn / nnpmc / variants).
+
+Env: ROWS (default 4096), NN_C (128 -> 128x10b, 256 -> 256x20b), NN_DTYPE
+(bf16 / fp16), AB_REF (save the outputs there on the first call, compare bit
+for bit on later ones), CHECK_REF=1 (max error of the first 256 rows against
+the fp32 restatement oracle/resnet_ref.py; test infrastructure, diagnostics).
+Prints one line: ms per launch (median of 5 x 10 launches), TFLOP/s."""
 import os
 import sys
 from pathlib import Path
@@ -13,12 +18,12 @@ import torch  # noqa: E402
 import othello_mcts as om  # noqa: E402
 from othello_mcts.synthetic import alphazero_state_dict  # noqa: E402
 
-rows = int(os.environ.get("ROWS", "8192"))
-v = os.environ.get("OAMD_RESNET_ABLATE", "0")
-C = int(os.environ.get("NN_C", "128"))  # 128 -> 128x10b, 256 -> 256x20b
+rows = int(os.environ.get("ROWS", "4096"))
+C = int(os.environ.get("NN_C", "128"))
+dtype = os.environ.get("NN_DTYPE", "bf16")
 R = 9 if C == 128 else 19
 sd = alphazero_state_dict(1, 17, C, R, C)
-net = om.NativeNet(sd, device=0)
+net = om.NativeNet(sd, device=0, dtype=dtype)
 flops = 2.0 * 64 * 9 * C * (17 + 2 * R * C) + 2.0 * (64 * C * 3 + 128 * 65 + 64 * C + C)  # bench.py
 x = (torch.rand((rows, 17, 8, 8), generator=torch.Generator().manual_seed(7)) < 0.3).float().cuda()
 for _ in range(3):
@@ -35,17 +40,11 @@ for _ in range(5):
     ms.append(a.elapsed_time(b) / 10)
 ms.sort()
 t = ms[len(ms) // 2]
-# schedule variants must not change a bit: compare with the saved reference
 out = net(x)
 torch.cuda.synchronize()
 chk = ""
 ref_file = os.environ.get("AB_REF")
-if ref_file:
-    # variants that change the K order (OAMD_KPERM) have their own reference;
-    # every variant is also compared with the first (baseline) reference
-    base_file = ref_file
-    if "OAMD_KPERM=1" in os.environ.get("AB_FLAGS", ""):
-        ref_file = ref_file + ".kperm"
+if ref_file:  # schedule variants must not change a bit
     if not os.path.exists(ref_file):
         torch.save({k: t_.cpu() for k, t_ in out.items()}, ref_file)
         chk = " [saved reference outputs]"
@@ -53,14 +52,12 @@ if ref_file:
         ref = torch.load(ref_file, weights_only=True)
         same = all(torch.equal(ref[k], out[k].cpu()) for k in ref)
         chk = " [outputs bit-identical]" if same else " [OUTPUTS DIFFER]"
-    if ref_file != base_file and os.path.exists(base_file):
-        b = torch.load(base_file, weights_only=True)
-        chk += (f" [vs baseline max|dp|={(b['policy'] - out['policy'].cpu()).abs().max().item():.2e}"
-                f" max|dv|={(b['value'] - out['value'].cpu()).abs().max().item():.2e}]")
-if os.environ.get("CHECK_REF"):  # accuracy vs the fp32 restatement (oracle/resnet_ref.py), first 256 rows
+if os.environ.get("CHECK_REF"):
     sys.path.insert(0, str(ROOT / "oracle"))
     import resnet_ref  # noqa: E402
+
     ref = resnet_ref.forward(sd, x[:256])
     chk += (f" [vs fp32: max|dp|={(ref['policy'] - out['policy'][:256]).abs().max().item():.2e}"
             f" max|dv|={(ref['value'] - out['value'][:256]).abs().max().item():.2e}]")
-print(f"variant {v}: {t:.3f} ms/launch  {flops * rows / t / 1e9:.1f} TFLOP/s  (rows={rows}){chk}", flush=True)
+print(f"k_resnet {C}x{R + 1}b {dtype}: {t:.4f} ms/launch  {flops * rows / t / 1e9:.1f} TFLOP/s  (rows={rows}){chk}",
+      flush=True)
