@@ -145,6 +145,11 @@ struct oamd_engine {
     float* policy = nullptr;
     float* value = nullptr;
     uint8_t* flags = nullptr;
+    // evaluation lists of the native search (tree.hip append_rows): the rows of
+    // non-terminal leaves per pipeline group, and two counters per group (the
+    // round being evaluated, the next round's)
+    int32_t* rowlist = nullptr;
+    int32_t* rowcount = nullptr;
     float* explore_tab = nullptr;
     unsigned long long* counters = nullptr;
     int32_t* status_dev = nullptr;  // [0] games with pool overflow, [1] depth-capped games
@@ -282,6 +287,7 @@ struct oamd_engine {
         E.eps = cfg.dirichlet_epsilon;
         E.alpha = cfg.dirichlet_alpha;
         E.counters = counters;
+        E.rowlist = rowlist;
         return E;
     }
 
@@ -297,10 +303,12 @@ struct oamd_engine {
         dfree(policy);
         dfree(value);
         dfree(flags);
+        dfree(rowlist);
         int rc;
         if ((rc = dalloc(&leaf, rows)) || (rc = dalloc(&depth, rows)) || (rc = dalloc(&trans, rows)) ||
             (rc = dalloc(&path, rows * kMaxDepth)) || (rc = dalloc(&feat, rows * fw)) ||
-            (rc = dalloc(&policy, rows * 65)) || (rc = dalloc(&value, rows)) || (rc = dalloc(&flags, rows)))
+            (rc = dalloc(&policy, rows * 65)) || (rc = dalloc(&value, rows)) || (rc = dalloc(&flags, rows)) ||
+            (rc = dalloc(&rowlist, rows)))
             return rc;
         HIPCHK(hipMemset(policy, 0, rows * 65 * sizeof(float)));
         HIPCHK(hipMemset(value, 0, rows * sizeof(float)));
@@ -333,6 +341,8 @@ struct oamd_engine {
         dfree(policy);
         dfree(value);
         dfree(flags);
+        dfree(rowlist);
+        dfree(rowcount);
         dfree(explore_tab);
         dfree(counters);
         dfree(status_dev);
@@ -704,6 +714,7 @@ int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity,
     const size_t nodes = (size_t)num_games * node_capacity;
     if ((rc = dalloc(&e->link, nodes)) || (rc = dalloc(&e->stat, nodes)) || (rc = dalloc(&e->pos, nodes)) ||
         (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) || (rc = dalloc(&e->counters, 4)) ||
+        (rc = dalloc(&e->rowcount, 2 * kMaxPipeline)) ||
         (rc = dalloc(&e->status_dev, 2)) || (rc = dalloc(&e->info_dev, num_games)) || (rc = dalloc(&e->visits_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->q_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->spd_dev, (size_t)8 * (1 + 2 * kMaxHistory) * 64 + 8 * 65)) || (rc = e->alloc_rows()) ||
@@ -711,7 +722,8 @@ int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity,
         delete e;
         return rc;
     }
-    if (hipMemset(e->counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMemset(e->counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(e->rowcount, 0, 2 * kMaxPipeline * sizeof(int32_t)) != hipSuccess) {
         delete e;
         return fail(OAMD_RUNTIME, "engine init: counter memset failed");
     }
@@ -933,7 +945,12 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             const size_t r0 = (size_t)g0[k] * L;
             hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
             if (ev) HIPCHK(hipEventRecord(ev[0], st[k]));
-            launch_tree(E, st[k], s > 0, s < steps, T, B, g0[k], ng[k]);
+            // evaluation list of group k: round s fills counter s % 2 and zeroes
+            // the other one (which round s-1's launch, done by now, read); the
+            // final round zeroes counter 0 for the next search's round 0
+            int* cnt = e->rowcount + 2 * k;
+            launch_tree(E, st[k], s > 0, s < steps, T, B, g0[k], ng[k], 0, -1, s < steps ? cnt + (s & 1) : nullptr,
+                        s < steps ? cnt + ((s + 1) & 1) : cnt);
             if (ev) HIPCHK(hipEventRecord(ev[1], st[k]));
             if (s == steps) continue;
             // the groups' NN launches run one after another (OAMD_NN_ORDER)
@@ -950,8 +967,8 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             const int grows = ng[k] * L;
             const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
             for (int r = 0; r < grows; r += cb)
-                launch_resnet_packed(N, E.feat + (r0 + r) * E.FW, E.FW, E.H, std::min(cb, grows - r),
-                                     E.policy + (r0 + r) * 65, E.value + r0 + r, ns);
+                launch_resnet_packed(N, E.feat, E.FW, E.H, std::min(cb, grows - r), E.policy, E.value, ns,
+                                     E.rowlist + r0 + r, cnt + (s & 1), r);
             if (nn_timed) HIPCHK(hipEventRecord(ev[3], ns));
             if (K > 1 && OAMD_NN_ORDER == 2) {
                 HIPCHK(hipEventRecord(e->nn_ev[k], ns));

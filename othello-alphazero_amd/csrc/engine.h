@@ -69,7 +69,8 @@ struct EngineView {
     float* value;    // G*L
     const float* explore_tab;  // kExploreTab
     float c_base, c_init, eps, alpha;
-    unsigned long long* counters;  // [0] sims, [1] evals
+    unsigned long long* counters;  // [0] sims, [1] evals (this search), [2] sims, [3] evals (cumulative)
+    int32_t* rowlist;  // G*L: evaluation lists (pipeline group k: from its first game's row)
 };
 
 }  // namespace oamd

@@ -21,9 +21,12 @@ struct SelfplayParams {
 // One search round for games [g0, g0 + ng) (ng < 0: to the end): for each
 // virtual thread t in [t0, t1) (t1 < 0: T), back up its previous batch
 // (do_backup), then select its next B leaves (do_select). T * B must equal
-// E.L. See tree.hip k_tree.
+// E.L. cnt_add: append the selected non-terminal rows to the evaluation list
+// E.rowlist[g0 * L ..] behind this counter; cnt_reset: the counter to zero
+// (the next round's). See tree.hip k_tree.
 void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
-                 int g0 = 0, int ng = -1, int t0 = 0, int t1 = -1);
+                 int g0 = 0, int ng = -1, int t0 = 0, int t1 = -1, int* cnt_add = nullptr,
+                 int* cnt_reset = nullptr);
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s);
 void launch_set_evaluation(const EngineView& E, const float* pol, const float* val, int row_begin,
                            int rows, hipStream_t s);
@@ -58,9 +61,13 @@ struct NetView {
     const uint16_t* hconv;  // 1x1 head convs (BN folded), MFMA A fragments: [C/32][lane][8]
 };
 
-// features: packed engine rows (fw words per row, history H) or fp32 planes
+// features: packed engine rows (fw words per row, history H) or fp32 planes.
+// Packed rows with an evaluation list (rowlist != nullptr): the launch
+// evaluates rows rowlist[0 .. min(rows, *rowcount - list_off)) (absolute row
+// indices into feat / policy / value); without one, rows 0 .. rows-1.
 void launch_resnet_packed(const NetView& N, const uint64_t* feat, int fw, int H, int rows,
-                          float* policy, float* value, hipStream_t s);
+                          float* policy, float* value, hipStream_t s, const int32_t* rowlist = nullptr,
+                          const int32_t* rowcount = nullptr, int list_off = 0);
 void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* policy, float* value,
                        hipStream_t s);
 size_t resnet_packed_weight_elems(int C, int R);

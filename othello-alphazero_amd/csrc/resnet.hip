@@ -10,8 +10,8 @@
 //     the A operand: an accumulator lane then holds 4 consecutive output
 //     channels of one position, so the epilogue writes 8 contiguous bytes;
 //     throughput geometries: wave (wm, wn) owns 32 channels (wn) x rows 0-7
-//     of board pair wm (OAMD_WIDE, edge tiling below); small-batch geometry:
-//     C/8 channels x the 64 positions of the board;
+//     of board pair wm (edge-row tiles, see wide_cb / edge_tile_row);
+//     small-batch geometry: C/8 channels x the 64 positions of the board;
 //   * K is walked in K-steps of one tap x 32 input channels. Weights (BatchNorm
 //     folded, packed on the host in fragment order) stream once per workgroup
 //     through a 3-slot LDS ring by LDS-DMA (global_load_lds_dwordx4); a 16 KiB
@@ -27,8 +27,9 @@
 //   * accumulators start from the folded bias (+ the residual skip for the
 //     second conv of a block, carried in registers from the first conv's
 //     epilogue), so the epilogue is cvt_pk + packed-i16 ReLU + one ds_write_b64;
-//   * heads (1x1 convs, Linear layers, softmax(65), tanh) run in fp32 on VALU,
-//     one wave per (board, head).
+//   * heads: both 1x1 convs of a board as one small MFMA GEMM, the Linear
+//     layers k-split in fp32 over every board of the workgroup, softmax(65),
+//     tanh (heads()).
 
 #include <hip/hip_runtime.h>
 
@@ -51,185 +52,38 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// Output channels per wave (OAMD_WC): 64 -> 8 waves of 64ch x 64 positions,
-// 2 per SIMD; 128 -> 4 waves of 128ch x 64 positions, one per SIMD, with 0.375
-// instead of 0.5 fragment reads per MFMA.
-#ifndef OAMD_WC
-#define OAMD_WC 64
-#endif
-// C=256 (2 boards per workgroup, one K-step per 16 KiB stage): 64-channel wave
-// tiles (8 waves, 2 per SIMD) take 7.56 ms per 4096 rows of 256x20b against
-// 8.19-8.21 with 128-channel tiles (4 waves) under the max-ILP scheduler
-// (round 2, two same-box pairs, bit-identical; round 1's default scheduler
-// had ranked them the other way, 7.8 %)
-#ifndef OAMD_WC256
-#define OAMD_WC256 64
-#endif
 constexpr int kLdsBytes = 160 * 1024;
+#ifdef OAMD_STAMPS
 constexpr int kMaxStampWgs = 1 << 16;
-// Weight stage = 16 KiB (2 K-steps at C=128, 1 at C=256) in a 3-slot ring.
-// Compile-time schedule knobs, A/B-measured on MI355X with tools/ab.sh (same box,
-// k_resnet 8192 rows, C=128): 16 KiB stages beat 8 KiB stages in a 6-slot ring
-// (4 stages in flight) by 3 %; the per-step fence (OAMD_FENCE) gains 2 %;
-// forcing reads before MFMAs (OAMD_READS_FIRST), placing the DMA between MFMAs
-// (OAMD_DMA_LATE) and s_setprio around MFMA runs (OAMD_PRIO) each lose 1-4 %;
-// issuing the activation fragments before the stage barrier (OAMD_XEARLY)
-// gains 3.6 %; 128-channel wave tiles (OAMD_WC=128, one wave per SIMD) lose 3 %;
-// a fine interleave, one fragment read then 4 MFMAs (OAMD_ILV=1), gains 2.5 %.
-#ifndef OAMD_STAGE128
-#define OAMD_STAGE128 16384
 #endif
-#ifndef OAMD_PRIO
-#define OAMD_PRIO 0
-#endif
-#ifndef OAMD_READS_FIRST
-#define OAMD_READS_FIRST 0
-#endif
-#ifndef OAMD_FENCE
-#define OAMD_FENCE 1
-#endif
-#ifndef OAMD_DMA_LATE
-#define OAMD_DMA_LATE 0
-#endif
-#ifndef OAMD_XEARLY
-#define OAMD_XEARLY 1
-#endif
-#ifndef OAMD_ILV
-#define OAMD_ILV 1
-#endif
-// epilogue: wait for the next layer's first weight stage before the first
-// barrier and read its weight fragments during the stores
-#ifndef OAMD_EPI_WEARLY
-#define OAMD_EPI_WEARLY 0  // measured +0.4 % (6 VGPRs spill under the 208 cap)
-#endif
+// Weight stream: 16 KiB stages (2 K-steps at C=128, 1 at C=256) in a 3-slot
+// LDS ring (the small-batch geometry: 4 slots), refilled by LDS-DMA. 8 KiB
+// stages in a 6-slot ring measured 3 % slower (DESIGN.md §6 lists every
+// measured alternative: register staging, early stage opening, staggered or
+// prioritised waves, other DMA placements, 128-channel tiles, ...).
+constexpr int kStageBytes = 16384;
+// k_resnet_w8 register cap: gfx950 counts the unified VGPR+AGPR file, the
+// backend doubles this value: 2 x 104 = 208 VGPRs, so one 96-VGPR k_tree wave
+// fits beside the two ResNet waves of a SIMD
 #ifndef OAMD_VGPR_CAP
-#define OAMD_VGPR_CAP 104  // gfx950 counts the unified VGPR+AGPR file: 2 x 104 = 208
+#define OAMD_VGPR_CAP 104
 #endif
-// MFMAs of a step over which OAMD_ILV=1 spreads the step's fragment reads
-#ifndef OAMD_ILV_SPAN
-#define OAMD_ILV_SPAN 16
-#endif
-#ifndef OAMD_DEEP_DMA
-#define OAMD_DEEP_DMA 1
-#endif
-// weight stream by register staging (global_load_dwordx4 -> VGPRs -> ds_write_b128
-// one stage later) instead of LDS-DMA, in a 2-slot ring
-#ifndef OAMD_REGSTAGE
-#define OAMD_REGSTAGE 0
-#endif
-static_assert(!OAMD_DEEP_DMA || OAMD_FENCE, "the deep weight ring relies on the per-step lgkmcnt(0) fence");
-// Who issues a stage's LDS-DMA pieces (throughput geometry at C=128: 8 waves,
-// 2 pieces per wave and stage, 2 K-steps per stage; other geometries use 0):
-//   0  every wave issues its 2 pieces at the stage-opening barrier
-//   1  every wave issues 1 piece at the opening step and 1 at the stage's
-//      second K-step (the two partners of a SIMD never stall in DMA issue for
-//      a whole step together)
-//   2  alternating halves: waves 0-3 issue all pieces of even stages, waves
-//      4-7 of odd stages (4 each), so one wave of every SIMD pair issues MFMAs
-//      while its partner issues DMA
-//   3  both pieces at the stage's second K-step: no DMA issue between the
-//      stage barrier and the weight-fragment reads behind it
-#ifndef OAMD_DMA_MODE
-#define OAMD_DMA_MODE 1  // same box, 4096 rows: 0.887-0.901 vs 0.909-0.921 ms (mode 0), bit-identical
-#endif
-// modes 1/3: pin the second K-step's DMA issue after this many of its
-// fragment reads (0 = leave the placement to the scheduler)
-#ifndef OAMD_DMA_PIN
-#define OAMD_DMA_PIN 0
-#endif
-// s_setprio 1 for waves 4-7 (the SIMD partners dispatched second) for the
-// whole tower, no per-segment flips (MI355X_MICROARCH.md, two waves per SIMD 4)
-#ifndef OAMD_PRIO_STATIC
-#define OAMD_PRIO_STATIC 0
-#endif
-// Early stage opening (throughput geometry at C=128): the barrier that opens
-// stage g+1 moves from the step that loads g+1's first K-step to the step
-// that loads stage g's second K-step, behind that step's fragment reads. The
-// weight reads of a new stage then never wait on a barrier, and the DMA issued
-// at the barrier refills stage g-1's slot with stage g+2 (two steps of lead).
-// 1 = the whole stage is issued at the barrier, 2 = its second piece at the
-// next step.
-#ifndef OAMD_EARLY_OPEN
-#define OAMD_EARLY_OPEN 0
-#endif
-#ifndef OAMD_STAGGER
-#define OAMD_STAGGER 0
-#endif
-// Edge-row tiling with zero-tap skipping and the dy-sweep K order
-// (throughput geometries):
-//   * a 16-position MFMA tile is one board row of two boards, so at the three
-//     dy = -1 taps the row-0 tiles (and at dy = +1 the row-7 tiles) read only
-//     the zero border: their MFMAs are skipped (8.3 % of the tower's MFMAs).
-//     Waves 0-3 own rows 0-3, their SIMD partners 4-7 rows 4-7;
-//   * the tower's K order runs, per dx and pair of 32-channel blocks, the
-//     K-steps (cb, dy) = (c,-1) (c,+1) (c,0) (c+1,0) (c+1,-1) (c+1,+1): every
-//     (-1,+1) stage holds one skip for each half, so all waves reach each
-//     stage barrier with the same work, and tile m at dy reads board row
-//     m + dy of its half, so a channel block's 3 taps of one dx read 6
-//     distinct rows, held in a register window: 6 activation-fragment reads
-//     instead of 12;
-//   * the order is one function shared by the host weight packer and every
-//     geometry (the small-batch one reads every fragment), so all geometries
-//     stay bit-identical;
-//   * C=256 below (OAMD_SWEEP256).
-// k_resnet_w8, 4096 rows, same box: tap-major 0.887-0.895 ms -> pair order
-// (tap a with a + 6 per stage, skips only) 0.868-0.872 -> sweep 0.941 vs 0.996
-// on a slow box (-5.6 %); tools/ab_prebuilt.sh, profiles/r02/.
-#ifndef OAMD_EDGE
-#define OAMD_EDGE 1
-#endif
-// C=256 (one K-step per 16 KiB stage, 2 boards per workgroup): the sweep
-// order and window too, and the skips although a stage cannot balance them
-// (each half skips in every other stage): 4096 rows of 256x20b, same box,
-// 7.88-7.93 ms tap-major -> 7.54 sweep -> 7.33 with skips (-7.4 %)
-#ifndef OAMD_SWEEP256
-#define OAMD_SWEEP256 1
-#endif
-#ifndef OAMD_SKIP_KS1
-#define OAMD_SKIP_KS1 1
-#endif
-// OAMD_WIDE (C=128): 32-channel x 128-position wave tiles (rows 0-7 of a
-// board pair, 8 MFMA tiles), K order (cb, dy) = (c,-1) (c,0) (c,+1) per dx,
-// an 8-row window: half the weight-fragment reads per MFMA, and every wave
-// skips the same border tiles (0 at dy = -1, 7 at dy = +1) at compile time
-#ifndef OAMD_WIDE
-#define OAMD_WIDE 1
-#endif
-// the same at C=256 (8 waves x 32 channels over both boards of a workgroup)
-#ifndef OAMD_WIDE256
-#define OAMD_WIDE256 1
-#endif
-__host__ __device__ constexpr bool kWideOrder(int C) {
-    return OAMD_EDGE != 0 && ((C == 128 && OAMD_WIDE) || (C == 256 && OAMD_WIDE256));
-}
-__host__ __device__ constexpr bool kSweepOrder(int C) {
-    return OAMD_EDGE != 0 && !kWideOrder(C) && (C == 128 || (C == 256 && OAMD_SWEEP256));
-}
-__host__ __device__ constexpr bool kEdgeOrder(int C) { return kSweepOrder(C) || kWideOrder(C); }
+// Tower K order and tiling (throughput geometries; DESIGN.md §6 "wide wave
+// tiles"): a wave owns 32 output channels x 128 positions, i.e. rows 0-7 of a
+// pair of boards (C=128) or of both boards (C=256), as 8 MFMA tiles of one
+// board row each (edge_tile_row). Per dx and 32-channel block the K-steps run
+// (cb, dy) = (c,-1) (c,0) (c,+1): tile m at dy reads board row m + dy, so the
+// three dy taps of one (dx, block) read the 8 board rows once into a register
+// window, and tile 0 at dy = -1 and tile 7 at dy = +1 read only the zero
+// border: those MFMAs are left out at compile time (8.3 % of the tower's).
+// The order is one function shared by the host weight packer and every
+// geometry (the small-batch one reads every fragment), so all geometries are
+// bit-identical.
 __host__ __device__ constexpr int wide_cb(int J) { return J / 3; }
 __host__ __device__ constexpr int wide_dy(int J) { return J % 3 - 1; }
 // window rows (bit i = board row i - 1) K-step J needs first: rows 0-6 at
 // dy = -1, row 7 at dy = 0
 __host__ __device__ constexpr int wide_new(int J) { return J % 3 == 0 ? 0xFE : (J % 3 == 1 ? 0x100 : 0); }
-// (cb, dy) of K-step J of a dx in the tower's order
-__host__ __device__ constexpr int ord_cb(int C, int J) { return kWideOrder(C) ? wide_cb(J) : J / 3; }
-__host__ __device__ constexpr int ord_dy(int C, int J) {
-    return kWideOrder(C) ? wide_dy(J) : ((J % 6 == 0 || J % 6 == 4) ? -1 : ((J % 6 == 1 || J % 6 == 5) ? 1 : 0));
-}
-// the sweep: (cb, dy) of the J-th K-step of a dx, and the window rows that
-// K-step J needs and no earlier K-step of its channel block has read
-__host__ __device__ constexpr int sweep_cb(int J) { return J / 3; }
-__host__ __device__ constexpr int sweep_dy(int J) {
-    return (J % 6 == 0 || J % 6 == 4) ? -1 : ((J % 6 == 1 || J % 6 == 5) ? 1 : 0);
-}
-__host__ __device__ constexpr int sweep_new(int J) {  // bit i = window row i (board row i - 1 + 4 * half)
-    return J % 6 == 0 ? 0x0F : (J % 6 == 1 ? 0x30 : (J % 6 == 2 ? 0 : (J % 6 == 3 ? 0x1E : (J % 6 == 4 ? 0x01 : 0x20))));
-}
-#ifndef OAMD_PRIO_ALL
-#define OAMD_PRIO_ALL 1  // s_setprio of every ResNet wave, throughput geometry (0 = off)
-#endif
-template <int C>
-__host__ __device__ constexpr int stage_bytes() { return C == 128 ? OAMD_STAGE128 : 16384; }
 
 // Head parameter buffer layout (fp32), filled by oamd_net_load_state (capi.hip).
 struct HeadLayout {
@@ -253,7 +107,7 @@ size_t resnet_head_floats(int C, int hidden) { return (size_t)HeadLayout(C, hidd
 
 // ---- K-step schedule (shared with the host packer) --------------------------
 __host__ __device__ constexpr int ksteps_per_stage(int C) {
-    return (C == 128 ? stage_bytes<128>() : stage_bytes<256>()) / (32 * C * 2);
+    return kStageBytes / (32 * C * 2);
 }
 __host__ __device__ constexpr int ksteps_first(int C) {
     return (9 + ksteps_per_stage(C) - 1) / ksteps_per_stage(C) * ksteps_per_stage(C);
@@ -267,14 +121,10 @@ void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad) {
         *tap = i < 9 ? i : 8;
         *cb = 0;
         *pad = i >= 9;
-    } else if (kSweepOrder(C) || kWideOrder(C)) {
+    } else {  // the tower's wide order: per dx, (cb, dy) = (c,-1) (c,0) (c,+1)
         const int dxi = i / (3 * (C / 32)), J = i % (3 * (C / 32));
-        *tap = dxi + 3 * (ord_dy(C, J) + 1);
-        *cb = ord_cb(C, J);
-        *pad = false;
-    } else {
-        *tap = i / (C / 32);
-        *cb = i % (C / 32);
+        *tap = dxi + 3 * (wide_dy(J) + 1);
+        *cb = wide_cb(J);
         *pad = false;
     }
 }
@@ -333,7 +183,7 @@ __host__ __device__ constexpr int edge_tile_row(int q, int m, int j) {
 // channels per wave (NT = WC/16 MFMA tiles), at most RING_MAX weight slots of
 // STAGE bytes (a whole number of K-steps; the packed weights are K-step
 // granular, so any stage size reads the same buffer).
-template <int C_, int BOARDS_, int WC_, int RING_MAX_, int STAGE_ = stage_bytes<C_>(), int PW_ = 64>
+template <int C_, int BOARDS_, int WC_, int RING_MAX_, int STAGE_ = kStageBytes, int PW_ = 64>
 struct GeoT {
     static constexpr int C = C_;
     static constexpr int BOARDS = BOARDS_;
@@ -348,10 +198,10 @@ struct GeoT {
     static constexpr int RP = 2 * C + 16;       // row pitch (bytes)
     // board stride in rows (10x10 padded board); with two boards per workgroup
     // 104, so the two boards of an edge tile sit 8 rows apart modulo 16
-    static constexpr int BROWS = BOARDS_ == 2 && kEdgeOrder(C_) ? 104 : 100;
+    static constexpr int BROWS = BOARDS_ == 2 ? 104 : 100;
     static constexpr int NPAIR = BOARDS / 2;
-    static constexpr bool EDGE = kEdgeOrder(C_) && BOARDS >= 2 && BOARDS % 2 == 0 && !OAMD_STAGGER &&
-                                 (kWideOrder(C_) ? (WC_ == 32 && PW_ == 128) : (WC_ == 64 && PW_ == 64)) &&
+    // edge-row wave tiles (32 channels x rows 0-7 of a board pair)
+    static constexpr bool EDGE = BOARDS >= 2 && BOARDS % 2 == 0 && WC_ == 32 && PW_ == 128 &&
                                  (STAGE_ == 2 * 32 * C_ * 2 || STAGE_ == 32 * C_ * 2);
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
     static constexpr int KSTEP_BYTES = 32 * C * 2;
@@ -364,54 +214,39 @@ struct GeoT {
     // The barrier that opens stage s issues stage s + AHEAD. Every wave has
     // retired its reads of stage s-1 before that barrier (the per-step
     // lgkmcnt(0) fence), so s-1's slot is free and AHEAD = RING - 1 stages fly
-    // while one is read (OAMD_DEEP_DMA=0: RING - 2, no reliance on the fence).
-    static constexpr int AHEAD = OAMD_DEEP_DMA ? RING - 1 : RING - 2;
-    static constexpr bool EARLY = OAMD_EARLY_OPEN && WAVES == 8 && KS == 2 && DPT == 2 && RING == 3 &&
-                                  !OAMD_REGSTAGE && !OAMD_STAGGER && OAMD_DEEP_DMA;
-    static constexpr bool EARLY_SPLIT = EARLY && OAMD_EARLY_OPEN == 2;
-    static constexpr int DMA_MODE = (WAVES == 8 && KS == 2 && DPT == 2 && !OAMD_REGSTAGE && !EARLY) ? OAMD_DMA_MODE : 0;
-    // vmcnt at a stage-opening barrier (mode 2: for the half that issued the
-    // stage being opened; the other half need not wait, VM_OPEN_OTHER)
-    static constexpr int VM_OPEN = DMA_MODE == 2 ? 0 : (AHEAD - 1) * DPT;
-    static constexpr int VM_OPEN_OTHER = DMA_MODE == 2 ? 2 * DPT : VM_OPEN;
-    // vmcnt after an epilogue's (or the prologue's) extra issue: mode 1 has
-    // issued only the first piece of the newest stage
-    static constexpr int VM_LAYER = DMA_MODE == 1 ? AHEAD * DPT - 1 : (DMA_MODE == 3 ? (AHEAD - 1) * DPT : AHEAD * DPT);
-    // what an opening (prologue, epilogue, stage barrier) issues of stage
-    // s + AHEAD: -1 all of this wave's pieces, 0 the first, -2 nothing (the
-    // stage's second K-step issues the rest)
-    static constexpr int OPEN_PART = DMA_MODE == 1 ? 0 : (DMA_MODE == 3 ? -2 : -1);
-    static constexpr int MID_PART = DMA_MODE == 1 ? 1 : -1;  // modes 1 and 3 only
-    static_assert(RING >= (OAMD_REGSTAGE ? 2 : 3) && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
+    // while one is read.
+    static constexpr int AHEAD = RING - 1;
+    // SPLIT_DMA (8 waves, 2 K-steps per stage): a wave issues the first of its
+    // two LDS-DMA pieces of a stage at the barrier that opens the stage before
+    // it and the second one at that stage's second K-step, so the weight reads
+    // behind a barrier never queue behind two DMA issues (-2.5 %, DESIGN.md
+    // §6); otherwise all of a wave's pieces go out at the barrier.
+    static constexpr bool SPLIT_DMA = WAVES == 8 && KS == 2 && DPT == 2;
+    // vmcnt at a stage-opening barrier, and after an epilogue's (or the
+    // prologue's) issue: with SPLIT_DMA only the newest stage's first piece
+    static constexpr int VM_OPEN = (AHEAD - 1) * DPT;
+    static constexpr int VM_LAYER = SPLIT_DMA ? AHEAD * DPT - 1 : AHEAD * DPT;
+    // which of this wave's pieces an opening issues (-1 all, 0 the first) and
+    // the stage's second K-step issues (1, SPLIT_DMA only)
+    static constexpr int OPEN_PART = SPLIT_DMA ? 0 : -1;
+    static constexpr int MID_PART = 1;
+    static_assert(RING >= 3 && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
     static_assert(ksteps_first(C) % KS == 0 && ksteps_tower(C) % KS == 0, "whole stages per layer");
     static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 63, "decomposition");
     static_assert(!EDGE || ((NPAIR * BROWS) % 16 == 8 && WAVES == 8), "edge tiles: pair boards 8 rows apart mod 16");
 };
-// throughput geometry: 512 positions x C channels per workgroup, 8 waves
+// throughput geometry: 512 positions x C channels per workgroup, 8 waves of
+// 32 channels x 128 positions (edge-row tiles)
 template <int C>
-using Geo = GeoT<C, 512 / C, kWideOrder(C) ? 32 : (C == 256 ? OAMD_WC256 : OAMD_WC), OAMD_REGSTAGE ? 2 : 3,
-                 stage_bytes<C>(), kWideOrder(C) ? 128 : 64>;
-// small-batch geometry (latency): one board per workgroup, 4 waves of C/4
-// channels, so a handful of rows spreads over as many CUs as boards; the LDS
-// ring depth (4, 6 or 8 slots) measured equal: at 8 MFMAs per wave and K-step
-// the per-step synchronisation, not the weight stream, bounds this geometry
-#ifndef OAMD_SMALL_RING
-#define OAMD_SMALL_RING 4
-#endif
-// waves per board in the small-batch geometry: 8 (16 channels each at C=128)
-// take 0.098 ms per 16-32 rows against 0.107 with 4 (tools/small_ab.sh, two
-// same-box pairs, bit-identical): in this latency regime the per-K-step chain
-// of one wave, not the fragment reads per MFMA, sets the time
-#ifndef OAMD_SMALL_WC_DIV
-#define OAMD_SMALL_WC_DIV 8
-#endif
+using Geo = GeoT<C, 512 / C, 32, 3, kStageBytes, 128>;
+// small-batch geometry (latency): one board per workgroup, 8 waves of C/8
+// channels, so a handful of rows spreads over as many CUs as boards. 8 waves
+// take 0.098 ms per 16-32 rows against 0.107 with 4 (two same-box pairs,
+// bit-identical): in this regime the per-K-step chain of one wave, not the
+// fragment reads per MFMA, sets the time; a 4-, 6- or 8-slot ring measured
+// equal
 template <int C>
-using GeoS = GeoT<C, 1, C / OAMD_SMALL_WC_DIV, OAMD_REGSTAGE ? 2 : OAMD_SMALL_RING>;
-// two workgroups per CU (C=128): 2 boards and 8 KiB stages per workgroup
-// (79 KB of LDS), so one workgroup's barriers and epilogues can overlap the
-// other's MFMAs, at twice the weight streaming per FLOP
-template <int C>
-using Geo2 = GeoT<C, 2, 64, 3, 8192>;
+using GeoS = GeoT<C, 1, C / 8, 4>;
 
 template <int DT>
 __device__ __forceinline__ uint32_t to_act(float v) {
@@ -457,6 +292,22 @@ __device__ __forceinline__ f32x4_t mfma(u32x4_t a, u32x4_t b, f32x4_t c) {
 
 enum InputKind { kPacked = 0, kF32 = 1 };
 
+// Rows of a launch: without a list, rows 0 .. rows-1; with the search's
+// evaluation list (tree.hip append_rows), entry i < rows is row list[i]. The
+// launch's grid covers the list's capacity; the entries filled this round are
+// counted on the device (resnet_body turns that count into `rows`).
+struct RowMap {
+    const int32_t* list;
+    const int32_t* count;  // filled entries + off (list entries before this launch)
+    int off;
+    int rows;
+};
+// row of launch entry r (= workgroup row0 + board), -1 past the end
+__device__ __forceinline__ int map_row(const RowMap& M, int r) {
+    if (r >= M.rows) return -1;
+    return M.list ? M.list[r] : r;
+}
+
 // Fragments of one K-step: 4 weight tiles (A: 16 channels x 32 K) and
 // 4 activation tiles (B: 32 K x 16 positions).
 template <int NT, int MT = 4>
@@ -465,48 +316,43 @@ struct Frags {
     u32x4_t x[MT];
 };
 
-// uniform byte offset of K-step i's rows/channels relative to the lane bases
+// uniform byte offset of the first conv's K-step i (tap-major, tap 8 repeated
+// as the zero-weight pad step) relative to the lane bases
 template <int C>
-__device__ __forceinline__ int kstep_offset(int i, bool first) {
-    int tap, cb;
-    if (first) {
-        tap = i < 9 ? i : 8;
-        cb = 0;
-    } else {
-        tap = i / (C / 32);
-        cb = i % (C / 32);
-    }
+__device__ __forceinline__ int first_kstep_offset(int i) {
+    const int tap = i < 9 ? i : 8;
     const int dy = tap / 3 - 1, dx = tap - 3 * (tap / 3) - 1;
-    return (dy * 10 + dx) * Geo<C>::RP + cb * 64;
+    return (dy * 10 + dx) * Geo<C>::RP;
+}
+// ... and of the tower's K-step 0 (dx = -1, dy = -1, channel block 0)
+template <int C>
+__device__ __forceinline__ int tower_kstep0_offset() {
+    return (-10 - 1) * Geo<C>::RP;
 }
 
 // ds_read the fragments of one K-step: wk = its weights in the ring (uniform),
-// aoff = kstep_offset (uniform); rd[m] / wl are per-lane bases
-template <int ABL = 0, int NT, int MT>
+// aoff = the K-step's uniform offset; rd[m] / wl are per-lane bases
+template <int NT, int MT>
 __device__ __forceinline__ void load_wfrags(Frags<NT, MT>& f, const unsigned char* wk, int wl) {
-    if constexpr (!(ABL & 4)) {
-        const unsigned char* wp = wk + wl;
+    const unsigned char* wp = wk + wl;
 #pragma unroll
-        for (int n = 0; n < NT; ++n) f.w[n] = *reinterpret_cast<const u32x4_t*>(wp + n * 1024);
-    }
+    for (int n = 0; n < NT; ++n) f.w[n] = *reinterpret_cast<const u32x4_t*>(wp + n * 1024);
 }
 
-template <int ABL = 0, int NT, int MT>
+template <int NT, int MT>
 __device__ __forceinline__ void load_xfrags(Frags<NT, MT>& f, const unsigned char* act, int aoff, const int (&rd)[MT]) {
-    if constexpr (ABL & 2) return;
     const unsigned char* ap = act + aoff;
 #pragma unroll
     for (int m = 0; m < MT; ++m) f.x[m] = *reinterpret_cast<const u32x4_t*>(ap + rd[m]);
 }
 
-template <int ABL = 0, int NT, int MT>
+template <int NT, int MT>
 __device__ __forceinline__ void load_frags(Frags<NT, MT>& f, const unsigned char* act, const unsigned char* wk,
                                            int aoff, const int (&rd)[MT], int wl) {
-    load_wfrags<ABL>(f, wk, wl);
-    load_xfrags<ABL>(f, act, aoff, rd);
+    load_wfrags(f, wk, wl);
+    load_xfrags(f, act, aoff, rd);
 }
 
-// half h of a K-step's MFMAs: output channel tiles n = 2h, 2h+1
 // f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>), in order
 template <int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -517,68 +363,29 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 template <int DT, int NT, int MT>
-__device__ __forceinline__ void mfma_half(f32x4_t (&acc)[NT][MT], const Frags<NT, MT>& f, int h) {
-#pragma unroll
-    for (int n = h * NT / 2; n < (h + 1) * NT / 2; ++n)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
-}
-
-template <int DT, int NT, int MT>
 __device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[NT][MT], const Frags<NT, MT>& f) {
-    if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
-    if constexpr (OAMD_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // Stages past the last one re-read the last stage into a slot nobody reads any
 // more: the issue stays branch-free and the vmcnt bookkeeping uniform.
 // PART: -1 = all of this wave's pieces of stage g; 0 / 1 = its first / second
-// piece (DMA_MODE 1). DMA_MODE 2: only the half owning stage g issues, 2 x DPT
-// pieces per wave.
+// piece (G::SPLIT_DMA).
 template <class G, int PART = -1>
 __device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsigned char* ring, int g, int slot,
                                                 int total, int tid) {
     const unsigned char* src = wsrc + (size_t)(g < total ? g : total - 1) * G::STAGE;
     unsigned char* dst = ring + slot * G::STAGE;
     const int wave = tid >> 6, lane = tid & 63;
-    if constexpr (PART == -2) {
-        return;
-    } else if constexpr (G::DMA_MODE == 2) {
-        if ((g & 1) != (wave >> 2)) return;  // wave-uniform
 #pragma unroll
-        for (int i = 0; i < 2 * G::DPT; ++i) {
-            const int q = (i * 4 + (wave & 3)) * 64;  // 1 KiB piece i*4 + wave%4
-            __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < G::DPT; ++i) {
-            if (PART >= 0 && i != PART) continue;
-            const int q = i * G::THREADS + wave * 64;  // first 16-byte chunk of this wave's piece
-            __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
-        }
+    for (int i = 0; i < G::DPT; ++i) {
+        if (PART >= 0 && i != PART) continue;
+        const int q = i * G::THREADS + wave * 64;  // first 16-byte chunk of this wave's piece
+        __builtin_amdgcn_global_load_lds(src + (size_t)(q + lane) * 16, (lds_void_t*)(dst + q * 16), 16, 0, 0);
     }
-}
-
-// register-staged weight stream: this thread's 16-byte chunks of stage g
-// (same linear chunk -> LDS mapping as the LDS-DMA path)
-template <class G>
-__device__ __forceinline__ void stage_load_regs(u32x4_t (&stg)[G::DPT], const unsigned char* wsrc, int g, int total,
-                                                int tid) {
-    const unsigned char* src = wsrc + (size_t)(g < total ? g : total - 1) * G::STAGE;
-#pragma unroll
-    for (int i = 0; i < G::DPT; ++i)
-        stg[i] = *reinterpret_cast<const u32x4_t*>(src + (size_t)(i * G::THREADS + tid) * 16);
-}
-template <class G>
-__device__ __forceinline__ void stage_store_lds(const u32x4_t (&stg)[G::DPT], unsigned char* ring, int slot, int tid) {
-    unsigned char* dst = ring + slot * G::STAGE;
-#pragma unroll
-    for (int i = 0; i < G::DPT; ++i) *reinterpret_cast<u32x4_t*>(dst + (i * G::THREADS + tid) * 16) = stg[i];
 }
 
 // s_waitcnt vmcnt(N): all but this wave's N youngest LDS-DMA / global ops done
@@ -658,7 +465,7 @@ __device__ __forceinline__ void dot32(float (&acc)[B], const float (&w)[32], con
 
 template <class G, int DT>
 __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act, unsigned char* scratch, int wave,
-                                      int lane, int row0, int rows, float* __restrict__ policy,
+                                      int lane, int row0, const RowMap& M, float* __restrict__ policy,
                                       float* __restrict__ value) {
     constexpr int C = G::C;
     constexpr int B = G::BOARDS;
@@ -757,8 +564,8 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
     OAMD_STAMP(10);
     for (int job = wave; job < 2 * B; job += NW) {
         const int b = job % B;
-        const int gr = row0 + b;
-        if (gr >= rows) continue;
+        const int gr = map_row(M, row0 + b);
+        if (gr < 0) continue;
         if (job < B) {
             const float o = hp[HL.plb + lane] + (((pp[(0 * B + b) * 64 + lane] + pp[(1 * B + b) * 64 + lane]) +
                                                   pp[(2 * B + b) * 64 + lane]) +
@@ -807,13 +614,8 @@ __device__ __forceinline__ void load_bias(float4 (&bv)[G::NT], const NetView& N,
                                                  (lane >> 4) * 4);
 }
 
-// ABL != 0 only in diagnostic ablation builds (OAMD_RESNET_ABLATE, wrong results):
-// bit 0 = no in-loop barrier/DMA wait, 1 = no activation fragment reads,
-// 16 = no epilogue stores (accumulators keep running into the next layer),
-// 2 = no weight fragment reads, 3 = no in-loop weight DMA, 5 (32) = no heads
-
-template <class G, int DT, int IN, int ABL = 0>
-__device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ feat_in, int fw, int H, int rows,
+template <class G, int DT, int IN>
+__device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ feat_in, int fw, int H, RowMap M,
                                             float* __restrict__ policy, float* __restrict__ value) {
     constexpr int C = G::C;
     constexpr int kNT = G::NT;
@@ -825,10 +627,14 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
-    const int wm = wave / G::WN;  // board of this wave (EDGE: position group, edge_tile_row)
-    const int wn = wave % G::WN;  // OAMD_WC-channel block of this wave
+    const int wm = wave / G::WN;  // position group of this wave (EDGE: edge_tile_row; else its board)
+    const int wn = wave % G::WN;  // 32-channel block of this wave
     const int kg = lane >> 4;
     const int row0 = blockIdx.x * G::BOARDS;
+    if (M.list) {  // entries filled this round (a uniform scalar load)
+        const int filled = *M.count - M.off;
+        M.rows = filled < M.rows ? (filled > 0 ? filled : 0) : M.rows;
+    }
     OAMD_STAMP(0);
 #ifdef OAMD_STAMPS
     // epilogue cycle sums: first barrier, stores, second barrier + first reads
@@ -847,27 +653,11 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
     const int total = (ksteps_first(C) + 2 * N.R * ksteps_tower(C)) / G::KS;
 
-    // weight stream starts right away: stages 0 .. AHEAD (register staging:
-    // stages 0 and 1 go to LDS now, stage 2 waits in VGPRs)
-    u32x4_t stg[G::DPT];
-    if constexpr (OAMD_REGSTAGE) {
-        stage_load_regs<G>(stg, wsrc, 0, total, tid);
-        stage_store_lds<G>(stg, ring, 0, tid);
-        stage_load_regs<G>(stg, wsrc, 1, total, tid);
-        stage_store_lds<G>(stg, ring, 1 % G::RING, tid);
-        stage_load_regs<G>(stg, wsrc, 2, total, tid);
-    } else {
-        if constexpr (G::EARLY) {
-            // stages 0 and 1; stage 2 goes out at stage 0's barrier
-            issue_stage_dma<G>(wsrc, ring, 0, 0, total, tid);
-            issue_stage_dma<G>(wsrc, ring, 1, 1, total, tid);
-        } else {
+    // weight stream starts right away: stages 0 .. AHEAD (with SPLIT_DMA the
+    // newest stage's second piece goes out at stage 0's second K-step)
 #pragma unroll
-            for (int s = 0; s < G::AHEAD; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
-            // mode 1: the newest stage's second piece goes out at stage 0's second K-step
-            issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, G::AHEAD, G::AHEAD, total, tid);
-        }
-    }
+    for (int s = 0; s < G::AHEAD; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
+    issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, G::AHEAD, G::AHEAD, total, tid);
 
     float4 bv[kNT];  // folded bias of this lane's output channels (current layer)
     load_bias<G>(bv, N, 0, wn, lane);
@@ -893,14 +683,14 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     }
     if (tid < G::BOARDS * 64) {
         const int b = tid >> 6, p = tid & 63;
-        const int gr = row0 + b;
+        const int gr = map_row(M, row0 + b);
         const uint32_t one = to_act<DT>(1.0f);
         uint32_t words[16];  // 32 channels as 16-bit pairs
         // one global round trip per board: the wave of board b (lane = square)
         // issues all its input loads before using any of them
         if constexpr (IN == kPacked) {
             uint32_t mask = 0;  // bit c = channel c is 1 (c < 31)
-            if (gr < rows) {    // wave-uniform
+            if (gr >= 0) {      // wave-uniform
                 // lane j holds word j of the row (fw = 2 + 2H <= 32 words)
                 const uint64_t* fr = reinterpret_cast<const uint64_t*>(feat_in) + (size_t)gr * fw;
                 const uint64_t wj = fr[p < fw ? p : fw - 1];
@@ -930,7 +720,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             float v[32];
 #pragma unroll
             for (int c = 0; c < 32; ++c) v[c] = 0.0f;
-            if (gr < rows) {  // wave-uniform; channel index clamped so all 32 loads issue at once
+            if (gr >= 0) {  // wave-uniform; channel index clamped so all 32 loads issue at once
                 const float* fr = reinterpret_cast<const float*>(feat_in) + (size_t)gr * N.cin * 64;
 #pragma unroll
                 for (int c = 0; c < 32; ++c) v[c] = fr[(c < N.cin ? c : N.cin - 1) * 64 + p];
@@ -954,12 +744,11 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     u32x2_t skip[kNT][kMT];  // residual (block input) of this lane's outputs
 
     Frags<kNT, kMT> fa, fb;
-    // dy-sweep order (G::EDGE && kSweepOrder): activation fragments of the
-    // current / next channel block by window row (fa / fb then carry weights)
-    constexpr bool kSweep = G::EDGE && kSweepOrder(C);
-    constexpr bool kWide = G::EDGE && kWideOrder(C);
-    u32x4_t win0[kWide ? 9 : 6], win1[kWide ? 9 : 6];
-    // window base: this lane's column, board row -1 (+ 4 x half), dx = -1
+    // edge-row tiles: the activation fragments of the current / next channel
+    // block come from register windows of board rows (fa / fb carry weights)
+    constexpr bool kWide = G::EDGE;
+    u32x4_t win0[kWide ? 9 : 1], win1[kWide ? 9 : 1];
+    // window base: this lane's column, board row -1, dx = -1
     const int sb0 = rd[0] - 10 * G::RP - G::RP;
     int g = 0;     // stage holding the current K-step
     int slot = 0;  // g % RING
@@ -975,28 +764,26 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         // released with the workgroup). Scalar loads of uniform addresses.
         bool live = false;
 #pragma unroll
-        for (int b = 0; b < G::BOARDS; ++b)
-            if (row0 + b < rows)
-                live |= ((reinterpret_cast<const uint64_t*>(feat_in)[(size_t)(row0 + b) * fw] >> 16) & 1ULL) != 0;
+        for (int b = 0; b < G::BOARDS; ++b) {
+            const int gr = map_row(M, row0 + b);
+            if (gr >= 0) live |= ((reinterpret_cast<const uint64_t*>(feat_in)[(size_t)gr * fw] >> 16) & 1ULL) != 0;
+        }
         if (!live) {
             wait_vm<0>();
             return;
         }
     }
     // stage 0 and the input planes must be visible (bias loads are older than the DMAs)
-    if constexpr (G::EARLY) wait_vm<G::DPT>();  // stage 0 landed (over-waits for stage 1: once)
-    else if constexpr (!OAMD_REGSTAGE) wait_vm<G::VM_LAYER>();
+    wait_vm<G::VM_LAYER>();
     lds_barrier();
-    load_frags(fa, act, ring, kstep_offset<C>(0, true), rd, wl);
+    load_frags(fa, act, ring, first_kstep_offset<C>(0), rd, wl);
     OAMD_STAMP(1);
-    if constexpr (OAMD_PRIO_STATIC && G::WAVES == 8)
-        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     // throughput geometry: every ResNet wave issues ahead of the other pipeline
     // group's co-resident tree waves (SQ arbitration): bench C2 4.42-4.47 vs
-    // 4.31-4.36 M sims/s (tools/bench_ab.sh, four same-box pairs on two boxes),
-    // launch 0.90-0.91 vs 0.92-0.935 ms (the standalone speed), the tree round
-    // 0.46 vs 0.34 ms and still hidden behind the other group's launch
-    if constexpr (OAMD_PRIO_ALL > 0 && G::BOARDS > 1) __builtin_amdgcn_s_setprio(OAMD_PRIO_ALL);
+    // 4.31-4.36 M sims/s (four same-box pairs on two boxes), launch 0.90-0.91
+    // vs 0.92-0.935 ms (the standalone speed), the tree round 0.46 vs 0.34 ms
+    // and still hidden behind the other group's launch
+    if constexpr (G::BOARDS > 1) __builtin_amdgcn_s_setprio(1);
 
     const int nlayers = 1 + 2 * N.R;
     // one conv layer: KIND 0 = first conv, 1 = a block's first conv (saves the
@@ -1006,8 +793,6 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         constexpr int kind = decltype(KIND)::value;
         constexpr bool first = kind == 0;
         constexpr int nk = first ? ksteps_first(C) : ksteps_tower(C);
-        // edge skipping: which wave half (SIMD partners) this wave is in
-        const int ehalf = __builtin_amdgcn_readfirstlane(wm / (G::NPAIR > 0 ? G::NPAIR : 1));
 
         // accumulators start at bias (+ block input for the block's second conv)
 #pragma unroll
@@ -1025,16 +810,11 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 acc[n][m] = a;
             }
 
-        // step: load K-step i1's fragments into nxt, then MFMAs on cur (K-step i1-1).
-        // NEW: i1 opens a new stage -> DMA wait + barrier, ring advances.
-        // GB = waves 4-7 (the SIMD partners of waves 0-3) with OAMD_STAGGER: half
-        // of cur's MFMAs go before the barrier, so while waves 0-3 issue the
-        // post-barrier DMA and reads, their partners keep the MFMA pipe busy
+        // step: load K-step i1's fragments into nxt, then MFMAs on cur (K-step
+        // i1-1). NEW: i1 opens a new stage -> DMA wait + barrier, ring advances.
         // xoff: uniform byte offset of the next K-step's activation rows/channels
-        auto step = [&](auto NEW, auto GB, const Frags<kNT, kMT>& cur, Frags<kNT, kMT>& nxt, int xoff) {
+        auto step = [&](auto NEW, const Frags<kNT, kMT>& cur, Frags<kNT, kMT>& nxt, int xoff) {
             constexpr bool open = decltype(NEW)::value;
-            constexpr bool gb = decltype(GB)::value;
-#if OAMD_FENCE
             // keep each step's MFMAs (on cur) with the fragment reads they hide:
             // without this fence the scheduler may hoist the next step's MFMAs over
             // the barrier right behind their reads and drain lgkmcnt each step
@@ -1043,69 +823,20 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             // issuing nxt's, or 16 outstanding reads overflow the 4-bit lgkmcnt
             // and the compiler drains nxt's reads too
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-#endif
-            if constexpr (gb) {
-                mfma_half<DT>(acc, cur, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if constexpr (G::EARLY) {
-                if constexpr (open) {
-                    // first K-step of stage g+1, opened by the previous step's barrier
-                    ++g;
-                    slot = slot == G::RING - 1 ? 0 : slot + 1;
-                    if constexpr (G::EARLY_SPLIT && !(ABL & 8)) {
-                        const int sa = slot == G::RING - 1 ? 0 : slot + 1;
-                        issue_stage_dma<G, 1>(wsrc, ring, g + 1, sa, total, tid);
-                    }
-                    load_wfrags<ABL>(nxt, ring + slot * G::STAGE, wl);
-                    load_xfrags<ABL>(nxt, act, xoff, rd);
-                } else {
-                    // second K-step of stage g: its reads first, then the barrier
-                    // that opens stage g+1 (every wave's DMA of it has landed, and
-                    // every wave has retired its reads of stage g-1)
-                    load_xfrags<ABL>(nxt, act, xoff, rd);
-                    load_wfrags<ABL>(nxt, ring + slot * G::STAGE + G::KSTEP_BYTES, wl);
-                    if constexpr (!(ABL & 1)) {
-                        wait_vm<0>();
-                        __builtin_amdgcn_s_barrier();
-                    }
-                    if constexpr (!(ABL & 8)) {
-                        int sa = slot + 2;
-                        sa = sa >= G::RING ? sa - G::RING : sa;
-                        issue_stage_dma<G, G::EARLY_SPLIT ? 0 : -1>(wsrc, ring, g + 2, sa, total, tid);
-                    }
-                }
-            }
             // activation fragments do not depend on the stage barrier (the
-            // layer's input is fixed): with OAMD_XEARLY they are issued before
-            // it, so their latency overlaps the barrier wait
-            if constexpr (OAMD_XEARLY && !G::EARLY) load_xfrags<ABL>(nxt, act, xoff, rd);
-            int sp = 0;
-            if constexpr (open && !G::EARLY) {
+            // layer's input is fixed): issued before it, their latency overlaps
+            // the barrier wait (+3.6 %)
+            load_xfrags(nxt, act, xoff, rd);
+            if constexpr (open) {
                 // open stage g+1: it has landed (this wave's DMAs, then everyone's
                 // via the barrier) and stage g-1's slot is drained by all waves
-                if constexpr (!(ABL & 1)) {
-                    if constexpr (G::DMA_MODE == 2) {
-                        // the half that issued stage g+1 waits for it; the other
-                        // half has only stage g+2 in flight
-                        if (((g + 1) & 1) == (wave >> 2)) wait_vm<G::VM_OPEN>();
-                        else wait_vm<G::VM_OPEN_OTHER>();
-                    } else if constexpr (!OAMD_REGSTAGE) {
-                        wait_vm<G::VM_OPEN>();
-                    }
-                    __builtin_amdgcn_s_barrier();
-                }
-                sp = (slot + G::AHEAD + 1) % G::RING;  // (g + 1 + AHEAD) % RING
-                if constexpr (OAMD_REGSTAGE) {
-                    // stage g+2 into the slot stage g just left; fetch stage g+3
-                    stage_store_lds<G>(stg, ring, (slot + 2) % G::RING, tid);
-                    stage_load_regs<G>(stg, wsrc, g + 3, total, tid);
-                } else if constexpr (!(ABL & 8) && !OAMD_DMA_LATE) {
-                    issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
-                }
+                wait_vm<G::VM_OPEN>();
+                __builtin_amdgcn_s_barrier();
+                const int sp = (slot + G::AHEAD + 1) % G::RING;  // (g + 1 + AHEAD) % RING
+                issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
                 ++g;
                 slot = slot == G::RING - 1 ? 0 : slot + 1;
-            } else if constexpr ((G::DMA_MODE == 1 || G::DMA_MODE == 3) && !(ABL & 8) && !G::EARLY) {
+            } else if constexpr (G::SPLIT_DMA) {
                 // the rest of stage g + AHEAD (its slot, stage g-1's, was freed
                 // by the barrier that opened stage g)
                 int sa = slot + G::AHEAD;
@@ -1113,339 +844,152 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 issue_stage_dma<G, G::MID_PART>(wsrc, ring, g + G::AHEAD, sa, total, tid);
             }
             constexpr int kis = open ? 0 : 1;  // K-step within its stage
-            if constexpr (!G::EARLY) load_wfrags<ABL>(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
-            if constexpr (!OAMD_XEARLY && !G::EARLY) load_xfrags<ABL>(nxt, act, xoff, rd);
-            if constexpr (open && !(ABL & 8) && OAMD_DMA_LATE)
-                issue_stage_dma<G>(wsrc, ring, g + G::AHEAD, sp, total, tid);
-            if constexpr (gb) {
-                mfma_half<DT>(acc, cur, 1);
-            } else {
-                mfma_frags<DT>(acc, cur);
-            }
-#if OAMD_READS_FIRST
-            // issue the 8 fragment reads first, the stage DMA a few MFMAs later
-            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-            if constexpr (open && OAMD_DMA_LATE) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-                __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, gb ? 4 : 12, 0);
-            } else {
-                __builtin_amdgcn_sched_group_barrier(0x008, gb ? 8 : 16, 0);
-            }
-#endif
-#if OAMD_ILV
-            // fine interleave of the step's fragment reads with its 16 MFMAs: a
-            // stage-opening step has the 4 weight reads after the barrier (the
-            // activation reads precede it, OAMD_XEARLY), the other step all 8
-            if constexpr (!gb && kMT != 4) {
-                // other tile counts: the step's reads spread evenly over its MFMAs
-                constexpr int nds = open && OAMD_XEARLY && !G::EARLY ? kNT : kNT + kMT;
+            load_wfrags(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
+            mfma_frags<DT>(acc, cur);
+            // fine interleave of the step's fragment reads with its MFMAs (one
+            // read, then a share of the MFMAs; +2.5 %): a stage-opening step has
+            // only its weight reads after the barrier
+            if constexpr (kMT != 4) {
+                constexpr int nds = open ? kNT : kNT + kMT;
                 constexpr int nm = kNT * kMT;
                 static_for<nds>([&](auto I) {
                     constexpr int i = decltype(I)::value;
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * nm / nds - i * nm / nds, 0);
                 });
-            } else if constexpr (!gb) {
-                constexpr int nds = open && OAMD_XEARLY && !G::EARLY ? 4 : 8;
-                if constexpr (OAMD_ILV == 2 && open) __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
-                if constexpr (OAMD_ILV == 5 && open) {  // DMA after the first read + 4 MFMAs
+            } else {
+                constexpr int nds = open ? 4 : 8;
+                static_for<nds>([&](auto) {
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     __builtin_amdgcn_sched_group_barrier(0x008, 16 / nds, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x020, G::DPT, 0);
-                }
-                static_for<(OAMD_ILV == 4 ? nds / 2 : (OAMD_ILV == 5 && open ? nds - 1 : nds))>([&](auto I) {
-                    if constexpr (!open && OAMD_DMA_PIN > 0 && decltype(I)::value == OAMD_DMA_PIN &&
-                                  (G::DMA_MODE == 1 || G::DMA_MODE == 3))
-                        __builtin_amdgcn_sched_group_barrier(0x020, G::DMA_MODE == 1 ? 1 : G::DPT, 0);
-                    if constexpr (OAMD_ILV == 4) {
-                        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x008, 32 / nds, 0);
-                    } else if constexpr (OAMD_ILV == 3) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 16 / nds, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    } else {
-                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x008, OAMD_ILV_SPAN / nds, 0);
-                    }
                 });
-                // reads spread over the first OAMD_ILV_SPAN MFMAs only: the rest
-                // of the step's MFMAs cover the last read's latency before the
-                // next step's lgkmcnt(0) fence
-                if constexpr (OAMD_ILV == 1 && OAMD_ILV_SPAN != 16)
-                    __builtin_amdgcn_sched_group_barrier(0x008, kNT * 4 - nds * (OAMD_ILV_SPAN / nds), 0);
             }
-#endif
         };
         using NewOdd = std::integral_constant<bool, G::KS == 1>;  // K-step i1 odd
         using NewEven = std::integral_constant<bool, true>;       // K-step i1 even
-        auto kloop = [&](auto GB) {
-            if constexpr (first) {
-                int i = 0;
-                for (; i + 2 < nk; i += 2) {
-                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(i + 1, true));
-                    step(NewEven{}, GB, fb, fa, kstep_offset<C>(i + 2, true));
-                }
-                if constexpr (nk % 2 == 0) {
-                    step(NewOdd{}, GB, fa, fb, kstep_offset<C>(nk - 1, true));
-                    mfma_frags<DT>(acc, fb);
-                } else {
-                    mfma_frags<DT>(acc, fa);
-                }
-            } else {
-                // tower conv, unrolled by tap: KPT K-steps (channel blocks c) per
-                // tap; the tap's row offset is computed once, the channel block
-                // is an immediate on the fragment reads. K-step (t, c) is current,
-                // the step loads (t, c + 1) or (t + 1, 0).
-                constexpr int KPT = C / 32;
-                static_assert(KPT % 2 == 0, "ping-pong parity per tap");
-                auto tapoff = [](int t) { return ((t / 3 - 1) * 10 + (t - 3 * (t / 3) - 1)) * G::RP; };
-                auto tap_steps = [&](int t, auto LAST) {
-                    constexpr bool last = decltype(LAST)::value;
-                    const int to = tapoff(t), tn = last ? 0 : tapoff(t + 1);
-                    static_for<last ? KPT - 1 : KPT>([&](auto J) {
-                        constexpr int c = decltype(J)::value;
-                        // the loaded K-step t*KPT + c + 1 opens a stage when it is even
-                        using NEW = std::integral_constant<bool, G::KS == 1 || (c + 1) % 2 == 0>;
-                        const int xoff = c + 1 == KPT ? tn : to + (c + 1) * 64;
-                        if constexpr (c % 2 == 0) step(NEW{}, GB, fa, fb, xoff);
-                        else step(NEW{}, GB, fb, fa, xoff);
-                    });
-                };
-                if constexpr (kWide) {
-                    static_assert(kNT == 2 && kMT == 8 && KPT % 2 == 0 && (G::KS == 1 || G::KS == 2), "wide geometry");
-                    constexpr int NJ = 3 * KPT;  // K-steps per dx
-                    constexpr int RS = 10 * G::RP;  // one board row
-                    // K-step J = (cb J/3, dy J%3 - 1) of the dx: tiles mlo..mhi-1
-                    // from window rows m + 1 + dy (tile 0 at dy = -1 and tile 7 at
-                    // dy = +1 read the zero border: left out, every wave alike)
-                    auto wstep = [&](auto JJ, const Frags<kNT, kMT>& wc, Frags<kNT, kMT>& wn, int sbn) {
-                        constexpr int J = decltype(JJ)::value;
-                        constexpr int Jn = (J + 1) % NJ;
-                        constexpr bool open = G::KS == 1 || Jn % 2 == 0;
-                        constexpr int dy = wide_dy(J), cbn = wide_cb(Jn), nnew = __builtin_popcount(wide_new(Jn));
-                        constexpr int mlo = dy < 0 ? 1 : 0, mhi = dy > 0 ? 7 : 8;
-                        auto& Wc = [&]() -> u32x4_t(&)[9] {
-                            if constexpr (wide_cb(J) % 2 == 0) return win0; else return win1;
-                        }();
-                        auto& Wn = [&]() -> u32x4_t(&)[9] {
-                            if constexpr (cbn % 2 == 0) return win0; else return win1;
-                        }();
-                        __builtin_amdgcn_sched_barrier(0);
-                        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wc / Wc have landed
-                        static_for<9>([&](auto I) {
-                            constexpr int i = decltype(I)::value;
-                            if constexpr ((wide_new(Jn) >> i) & 1)
-                                Wn[i] = *reinterpret_cast<const u32x4_t*>(act + sbn + i * RS + cbn * 64);
-                        });
-                        if constexpr (open) {
-                            wait_vm<G::VM_OPEN>();
-                            __builtin_amdgcn_s_barrier();
-                            const int sp = (slot + G::AHEAD + 1) % G::RING;
-                            issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
-                            ++g;
-                            slot = slot == G::RING - 1 ? 0 : slot + 1;
-                        } else if constexpr (G::DMA_MODE == 1 || G::DMA_MODE == 3) {
-                            int sa = slot + G::AHEAD;
-                            sa = sa >= G::RING ? sa - G::RING : sa;
-                            issue_stage_dma<G, G::MID_PART>(wsrc, ring, g + G::AHEAD, sa, total, tid);
-                        }
-                        load_wfrags(wn, ring + slot * G::STAGE + (open ? 0 : G::KSTEP_BYTES), wl);
-#pragma unroll
-                        for (int n = 0; n < kNT; ++n)
-#pragma unroll
-                            for (int m = mlo; m < mhi; ++m) acc[n][m] = mfma<DT>(wc.w[n], Wc[m + 1 + dy], acc[n][m]);
-                        constexpr int nds = open ? kNT : kNT + nnew;
-                        constexpr int nm = kNT * (mhi - mlo);
-                        static_for<nds>([&](auto I) {
-                            constexpr int i = decltype(I)::value;
-                            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                            __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * nm / nds - i * nm / nds, 0);
-                        });
-                    };
-                    auto dx_wide = [&](int dxi, auto LASTDX) {
-                        constexpr bool lastdx = decltype(LASTDX)::value;
-                        const int sb = sb0 + dxi * G::RP;
-                        static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
-                            constexpr int J = decltype(JJ)::value;
-                            const int sbn = J == NJ - 1 ? sb + G::RP : sb;
-                            if constexpr (J % 2 == 0) wstep(JJ, fa, fb, sbn);
-                            else wstep(JJ, fb, fa, sbn);
-                        });
-                        if constexpr (lastdx) {
-                            // the layer's last K-step = (last block, dy +1) in fb / win1
-#pragma unroll
-                            for (int n = 0; n < kNT; ++n)
-#pragma unroll
-                                for (int m = 0; m < 7; ++m) acc[n][m] = mfma<DT>(fb.w[n], win1[m + 2], acc[n][m]);
-                        }
-                    };
-#pragma nounroll
-                    for (int dxi = 0; dxi < 2; ++dxi) dx_wide(dxi, std::false_type{});
-                    dx_wide(2, std::true_type{});
-                } else if constexpr (kSweep) {
-                    static_assert(kNT == 4 && KPT % 2 == 0 && (G::KS == 1 || G::KS == 2), "sweep geometry");
-                    constexpr int NJ = 3 * KPT;  // K-steps per dx
-                    constexpr bool SKIP = G::KS == 2 || OAMD_SKIP_KS1;
-                    constexpr int RS = 10 * G::RP;  // one board row
-                    // K-step J of the dx at sb (window base + dx): MFMAs from the
-                    // window, weights wc; reads the window rows K-step J + 1 needs
-                    // (at sbn: the next dx's base when J = 11) and its weights
-                    auto sstep = [&](auto JJ, const Frags<kNT, kMT>& wc, Frags<kNT, kMT>& wn, int sbn) {
-                        constexpr int J = decltype(JJ)::value;
-                        constexpr int Jn = (J + 1) % NJ;
-                        constexpr bool open = G::KS == 1 || Jn % 2 == 0;  // K-step J + 1 opens a stage
-                        constexpr int dy = sweep_dy(J), cbn = sweep_cb(Jn), nnew = __builtin_popcount(sweep_new(Jn));
-                        constexpr int tsk = !SKIP ? -1 : (dy < 0 ? 0 : (dy > 0 ? 3 : -1));  // border tile of one half
-                        auto& Wc = [&]() -> u32x4_t(&)[6] {
-                            if constexpr (sweep_cb(J) % 2 == 0) return win0; else return win1;
-                        }();
-                        auto& Wn = [&]() -> u32x4_t(&)[6] {
-                            if constexpr (cbn % 2 == 0) return win0; else return win1;
-                        }();
-                        __builtin_amdgcn_sched_barrier(0);
-                        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wc / Wc have landed
-                        // the next K-step's new window rows (do not depend on the barrier)
-                        static_for<6>([&](auto I) {
-                            constexpr int i = decltype(I)::value;
-                            if constexpr ((sweep_new(Jn) >> i) & 1)
-                                Wn[i] = *reinterpret_cast<const u32x4_t*>(act + sbn + i * RS + cbn * 64);
-                        });
-                        if constexpr (open) {
-                            wait_vm<G::VM_OPEN>();
-                            __builtin_amdgcn_s_barrier();
-                            const int sp = (slot + G::AHEAD + 1) % G::RING;
-                            issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
-                            ++g;
-                            slot = slot == G::RING - 1 ? 0 : slot + 1;
-                        } else if constexpr (G::DMA_MODE == 1 || G::DMA_MODE == 3) {
-                            int sa = slot + G::AHEAD;
-                            sa = sa >= G::RING ? sa - G::RING : sa;
-                            issue_stage_dma<G, G::MID_PART>(wsrc, ring, g + G::AHEAD, sa, total, tid);
-                        }
-                        load_wfrags(wn, ring + slot * G::STAGE + (open ? 0 : G::KSTEP_BYTES), wl);
-#pragma unroll
-                        for (int n = 0; n < kNT; ++n)
-#pragma unroll
-                            for (int m = 0; m < 4; ++m)
-                                if (m != tsk) acc[n][m] = mfma<DT>(wc.w[n], Wc[m + 1 + dy], acc[n][m]);
-                        constexpr int nds = open ? kNT : kNT + nnew;
-                        constexpr int nm = kNT * (tsk >= 0 ? 3 : 4);
-                        // reads spread evenly over the MFMAs (all reads first: +2-3 %)
-                        static_for<nds>([&](auto I) {
-                            constexpr int i = decltype(I)::value;
-                            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                            __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * nm / nds - i * nm / nds, 0);
-                        });
-                        if constexpr (tsk >= 0) {
-                            // waves 0-3 skip tile 0 at dy = -1, waves 4-7 tile 3 at dy = +1
-                            if (dy < 0 ? ehalf != 0 : ehalf == 0)
-#pragma unroll
-                                for (int n = 0; n < kNT; ++n)
-                                    acc[n][tsk] = mfma<DT>(wc.w[n], Wc[tsk + 1 + dy], acc[n][tsk]);
-                        }
-                    };
-                    auto dx_sweep = [&](int dxi, auto LASTDX) {
-                        constexpr bool lastdx = decltype(LASTDX)::value;
-                        const int sb = sb0 + dxi * G::RP;
-                        static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
-                            constexpr int J = decltype(JJ)::value;
-                            const int sbn = J == NJ - 1 ? sb + G::RP : sb;
-                            if constexpr (J % 2 == 0) sstep(JJ, fa, fb, sbn);
-                            else sstep(JJ, fb, fa, sbn);
-                        });
-                        if constexpr (lastdx) {
-                            // the layer's last K-step = (last block, dy +1) in fb / win1:
-                            // waves 4-7 skip tile 3
-#pragma unroll
-                            for (int n = 0; n < kNT; ++n)
-#pragma unroll
-                                for (int m = 0; m < 3; ++m) acc[n][m] = mfma<DT>(fb.w[n], win1[m + 2], acc[n][m]);
-                            if (!SKIP || ehalf == 0)
-#pragma unroll
-                                for (int n = 0; n < kNT; ++n) acc[n][3] = mfma<DT>(fb.w[n], win1[5], acc[n][3]);
-                        }
-                    };
-#pragma nounroll
-                    for (int dxi = 0; dxi < 2; ++dxi) dx_sweep(dxi, std::false_type{});
-                    dx_sweep(2, std::true_type{});
-                } else if constexpr (kSweepOrder(C) || kWideOrder(C)) {
-                    // the tower's order without edge tiles (small-batch geometry):
-                    // generic steps, every K-step's fragments read
-                    static_assert(KPT % 2 == 0, "sweep: whole block pairs");
-                    constexpr int NJ = 3 * KPT;
-                    auto xoff_of = [](int dxi, int J) {
-                        return (ord_dy(C, J) * 10 + dxi - 1) * G::RP + ord_cb(C, J) * 64;
-                    };
-                    auto dx_steps = [&](int dxi, auto LASTDX) {
-                        constexpr bool lastdx = decltype(LASTDX)::value;
-                        static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
-                            constexpr int J = decltype(JJ)::value;
-                            using NEW = std::integral_constant<bool, G::KS == 1 || (J + 1) % 2 == 0>;
-                            const int xo = J == NJ - 1 ? xoff_of(dxi + 1, 0) : xoff_of(dxi, J + 1);
-                            if constexpr (J % 2 == 0) step(NEW{}, GB, fa, fb, xo);
-                            else step(NEW{}, GB, fb, fa, xo);
-                        });
-                    };
-#pragma nounroll
-                    for (int dxi = 0; dxi < 2; ++dxi) dx_steps(dxi, std::false_type{});
-                    dx_steps(2, std::true_type{});
-                    mfma_frags<DT>(acc, fb);  // the layer's last K-step
-                } else {
-                    for (int t = 0; t < 8; ++t) tap_steps(t, std::false_type{});
-                    tap_steps(8, std::true_type{});
-                    mfma_frags<DT>(acc, fb);  // K-step 9*KPT - 1 (odd c)
-                }
+        if constexpr (first) {
+            int i = 0;
+            for (; i + 2 < nk; i += 2) {
+                step(NewOdd{}, fa, fb, first_kstep_offset<C>(i + 1));
+                step(NewEven{}, fb, fa, first_kstep_offset<C>(i + 2));
             }
-        };
-        if constexpr (OAMD_STAGGER) {
-            if (wave >= 4) kloop(std::true_type{});
-            else kloop(std::false_type{});
+            if constexpr (nk % 2 == 0) {
+                step(NewOdd{}, fa, fb, first_kstep_offset<C>(nk - 1));
+                mfma_frags<DT>(acc, fb);
+            } else {
+                mfma_frags<DT>(acc, fa);
+            }
+        } else if constexpr (kWide) {
+            constexpr int KPT = C / 32;
+            static_assert(kNT == 2 && kMT == 8 && KPT % 2 == 0 && (G::KS == 1 || G::KS == 2), "wide geometry");
+            constexpr int NJ = 3 * KPT;     // K-steps per dx
+            constexpr int RS = 10 * G::RP;  // one board row
+            // K-step J = (cb J/3, dy J%3 - 1) of the dx: tiles mlo..mhi-1 from
+            // window rows m + 1 + dy (tile 0 at dy = -1 and tile 7 at dy = +1
+            // read the zero border: left out, every wave alike); reads the
+            // window rows K-step J + 1 needs (at sbn: the next dx's base when
+            // J = NJ - 1) and its weights
+            auto wstep = [&](auto JJ, const Frags<kNT, kMT>& wc, Frags<kNT, kMT>& wn, int sbn) {
+                constexpr int J = decltype(JJ)::value;
+                constexpr int Jn = (J + 1) % NJ;
+                constexpr bool open = G::KS == 1 || Jn % 2 == 0;
+                constexpr int dy = wide_dy(J), cbn = wide_cb(Jn), nnew = __builtin_popcount(wide_new(Jn));
+                constexpr int mlo = dy < 0 ? 1 : 0, mhi = dy > 0 ? 7 : 8;
+                auto& Wc = [&]() -> u32x4_t(&)[9] {
+                    if constexpr (wide_cb(J) % 2 == 0) return win0; else return win1;
+                }();
+                auto& Wn = [&]() -> u32x4_t(&)[9] {
+                    if constexpr (cbn % 2 == 0) return win0; else return win1;
+                }();
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wc / Wc have landed
+                static_for<9>([&](auto I) {
+                    constexpr int i = decltype(I)::value;
+                    if constexpr ((wide_new(Jn) >> i) & 1)
+                        Wn[i] = *reinterpret_cast<const u32x4_t*>(act + sbn + i * RS + cbn * 64);
+                });
+                if constexpr (open) {
+                    wait_vm<G::VM_OPEN>();
+                    __builtin_amdgcn_s_barrier();
+                    const int sp = (slot + G::AHEAD + 1) % G::RING;
+                    issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
+                    ++g;
+                    slot = slot == G::RING - 1 ? 0 : slot + 1;
+                } else if constexpr (G::SPLIT_DMA) {
+                    int sa = slot + G::AHEAD;
+                    sa = sa >= G::RING ? sa - G::RING : sa;
+                    issue_stage_dma<G, G::MID_PART>(wsrc, ring, g + G::AHEAD, sa, total, tid);
+                }
+                load_wfrags(wn, ring + slot * G::STAGE + (open ? 0 : G::KSTEP_BYTES), wl);
+#pragma unroll
+                for (int n = 0; n < kNT; ++n)
+#pragma unroll
+                    for (int m = mlo; m < mhi; ++m) acc[n][m] = mfma<DT>(wc.w[n], Wc[m + 1 + dy], acc[n][m]);
+                constexpr int nds = open ? kNT : kNT + nnew;
+                constexpr int nm = kNT * (mhi - mlo);
+                static_for<nds>([&](auto I) {
+                    constexpr int i = decltype(I)::value;
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * nm / nds - i * nm / nds, 0);
+                });
+            };
+            auto dx_wide = [&](int dxi, auto LASTDX) {
+                constexpr bool lastdx = decltype(LASTDX)::value;
+                const int sb = sb0 + dxi * G::RP;
+                static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
+                    constexpr int J = decltype(JJ)::value;
+                    const int sbn = J == NJ - 1 ? sb + G::RP : sb;
+                    if constexpr (J % 2 == 0) wstep(JJ, fa, fb, sbn);
+                    else wstep(JJ, fb, fa, sbn);
+                });
+                if constexpr (lastdx) {
+                    // the layer's last K-step = (last block, dy +1) in fb / win1
+#pragma unroll
+                    for (int n = 0; n < kNT; ++n)
+#pragma unroll
+                        for (int m = 0; m < 7; ++m) acc[n][m] = mfma<DT>(fb.w[n], win1[m + 2], acc[n][m]);
+                }
+            };
+#pragma nounroll
+            for (int dxi = 0; dxi < 2; ++dxi) dx_wide(dxi, std::false_type{});
+            dx_wide(2, std::true_type{});
         } else {
-            kloop(std::false_type{});
+            // the tower's order without edge tiles (small-batch geometry):
+            // generic steps, every K-step's fragments read
+            constexpr int KPT = C / 32;
+            static_assert(KPT % 2 == 0, "whole block pairs");
+            constexpr int NJ = 3 * KPT;
+            auto xoff_of = [](int dxi, int J) { return (wide_dy(J) * 10 + dxi - 1) * G::RP + wide_cb(J) * 64; };
+            auto dx_steps = [&](int dxi, auto LASTDX) {
+                constexpr bool lastdx = decltype(LASTDX)::value;
+                static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
+                    constexpr int J = decltype(JJ)::value;
+                    using NEW = std::integral_constant<bool, G::KS == 1 || (J + 1) % 2 == 0>;
+                    const int xo = J == NJ - 1 ? xoff_of(dxi + 1, 0) : xoff_of(dxi, J + 1);
+                    if constexpr (J % 2 == 0) step(NEW{}, fa, fb, xo);
+                    else step(NEW{}, fb, fa, xo);
+                });
+            };
+#pragma nounroll
+            for (int dxi = 0; dxi < 2; ++dxi) dx_steps(dxi, std::false_type{});
+            dx_steps(2, std::true_type{});
+            mfma_frags<DT>(acc, fb);  // the layer's last K-step
         }
 
         // ---------------- epilogue: ReLU, in place --------------------------
         // stages g+1 .. (next layer's) are in flight; the next layer's bias is
         // loaded before the next DMA so the counted wait below covers it
         const bool more = layer + 1 < nlayers;
-        constexpr bool wearly = OAMD_EPI_WEARLY && !OAMD_REGSTAGE;
-        if constexpr (wearly) {
-            // the next layer's first stage (g + 1) lands before the first
-            // barrier, so its weight fragments are read during the stores
-            if constexpr (!(ABL & 1)) wait_vm<(G::AHEAD - 1) * G::DPT>();
-        } else {
-            if (more) load_bias<G>(bv, N, layer + 1, wn, lane);
-        }
+        if (more) load_bias<G>(bv, N, layer + 1, wn, lane);
         OAMD_EP_MARK(0);
         lds_barrier();  // every wave is done reading this layer's input and stage g
         OAMD_EP_MARK(1);
-        if constexpr (G::EARLY) {
-            // stage g+1 was opened by the layer's last barrier; with the split
-            // issue, the second piece of stage g+2 goes out here
-            if constexpr (G::EARLY_SPLIT && !(ABL & 8)) {
-                int sa = slot + 2;
-                sa = sa >= G::RING ? sa - G::RING : sa;
-                issue_stage_dma<G, 1>(wsrc, ring, g + 2, sa, total, tid);
-            }
-        } else if constexpr (OAMD_REGSTAGE) {
-            stage_store_lds<G>(stg, ring, (slot + 2) % G::RING, tid);
-            stage_load_regs<G>(stg, wsrc, g + 3, total, tid);
-        } else {
-            issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, (slot + G::AHEAD + 1) % G::RING, total,
-                                             tid);
-        }
-        if constexpr (wearly) {
-            if (more) {
-                load_bias<G>(bv, N, layer + 1, wn, lane);
-                load_wfrags<ABL>(fa, ring + (slot == G::RING - 1 ? 0 : slot + 1) * G::STAGE, wl);
-            }
-        }
+        issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, (slot + G::AHEAD + 1) % G::RING, total,
+                                         tid);
 #pragma unroll
         for (int n = 0; n < kNT; ++n)
 #pragma unroll
             for (int m = 0; m < kMT; ++m) {
-                if constexpr (ABL & 16) continue;
                 u32x2_t* p = reinterpret_cast<u32x2_t*>(act + wr[m] + n * 32);
                 if constexpr (kind == 1) skip[n][m] = *p;  // block input, needed by conv2
                 const f32x4_t a = acc[n][m];
@@ -1455,37 +999,15 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         slot = slot == G::RING - 1 ? 0 : slot + 1;
         OAMD_EP_MARK(2);
         if (more) {
-            if constexpr (wearly) {
-                lds_barrier();  // this layer's output is complete
-                if constexpr (kSweep) {
+            // stage g has landed (later may fly)
+            wait_vm<G::VM_LAYER>();
+            lds_barrier();  // ... and this layer's output is complete
+            if constexpr (kWide) {
+                load_wfrags(fa, ring + slot * G::STAGE, wl);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
-                } else if constexpr (kWide) {
-#pragma unroll
-                    for (int i = 1; i < 8; ++i)
-                        win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
-                } else {
-                    load_xfrags<ABL>(fa, act, kstep_offset<C>(0, false), rd);
-                }
+                for (int i = 1; i < 8; ++i) win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
             } else {
-                // stage g has landed (later may fly); with EARLY the last barrier
-                // of the layer already waited for it
-                if constexpr (!OAMD_REGSTAGE && !G::EARLY) wait_vm<G::VM_LAYER>();
-                lds_barrier();           // ... and this layer's output is complete
-                if constexpr (kSweep) {
-                    load_wfrags<ABL>(fa, ring + slot * G::STAGE, wl);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
-                } else if constexpr (kWide) {
-                    load_wfrags<ABL>(fa, ring + slot * G::STAGE, wl);
-#pragma unroll
-                    for (int i = 1; i < 8; ++i)
-                        win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
-                } else {
-                    load_frags(fa, act, ring + slot * G::STAGE, kstep_offset<C>(0, false), rd, wl);
-                }
+                load_frags(fa, act, ring + slot * G::STAGE, tower_kstep0_offset<C>(), rd, wl);
             }
 #ifdef OAMD_STAMPS
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1499,129 +1021,85 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         conv(std::integral_constant<int, 2>{}, 2 + 2 * blk);
     }
     __syncthreads();  // also drains this wave's trailing ring DMAs: the ring is free
-    if constexpr (OAMD_PRIO_STATIC && G::WAVES == 8) __builtin_amdgcn_s_setprio(0);
     OAMD_STAMP(2);
 #ifdef OAMD_STAMPS
     if (wave == 0 && lane == 0 && blockIdx.x < kMaxStampWgs)
         for (int i = 0; i < 3; ++i) g_oamd_stamps[blockIdx.x * 16 + 11 + i] = ep_sum[i];
 #endif
-    if constexpr (ABL & 32) return;
-    heads<G, DT>(N, act, ring, wave, lane, row0, rows, policy, value);
+    heads<G, DT>(N, act, ring, wave, lane, row0, M, policy, value);
     OAMD_STAMP(3);
 }
 
-template <class G, int DT, int IN, int ABL = 0>
-__global__ __launch_bounds__(G::THREADS) void k_resnet(NetView N, const void* __restrict__ feat_in, int fw, int H,
-                                                    int rows, float* __restrict__ policy, float* __restrict__ value) {
-    resnet_body<G, DT, IN, ABL>(N, feat_in, fw, H, rows, policy, value);
-}
-// The 8-wave (2 per SIMD) geometry capped at 208 VGPRs: that leaves 96 of a
-// SIMD's 512 for one k_tree wave (<= 96 VGPRs, no LDS), so the other pipeline
-// group's tree kernel co-resides with this kernel instead of waiting for a CU.
-// amdgpu_num_vgpr counts in units of the unified VGPR+AGPR file on gfx950
-// (the backend doubles it), hence OAMD_VGPR_CAP = 104; build.py checks the
-// resulting allocation.
-template <class G, int DT, int IN, int ABL = 0>
+// Every geometry is 8 waves (2 per SIMD), capped at 208 VGPRs: that leaves 96
+// of a SIMD's 512 for one k_tree wave (<= 96 VGPRs, no LDS), so the other
+// pipeline group's tree kernel co-resides with this kernel instead of waiting
+// for a CU. amdgpu_num_vgpr counts in units of the unified VGPR+AGPR file on
+// gfx950 (the backend doubles it), hence OAMD_VGPR_CAP = 104; build.py checks
+// the resulting allocation.
+template <class G, int DT, int IN>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_num_vgpr(OAMD_VGPR_CAP))) void k_resnet_w8(
-    NetView N, const void* __restrict__ feat_in, int fw, int H, int rows, float* __restrict__ policy,
+    NetView N, const void* __restrict__ feat_in, int fw, int H, RowMap M, float* __restrict__ policy,
     float* __restrict__ value) {
-    resnet_body<G, DT, IN, ABL>(N, feat_in, fw, H, rows, policy, value);
+    resnet_body<G, DT, IN>(N, feat_in, fw, H, M, policy, value);
 }
 
-template <class G, int DT, int IN, int ABL = 0>
-static void launch_t(const NetView& N, const void* feat, int fw, int H, int rows, float* pol,
-                     float* val, hipStream_t s) {
+template <class G, int DT, int IN>
+static void launch_t(const NetView& N, const void* feat, int fw, int H, const RowMap& M, float* pol, float* val,
+                     hipStream_t s) {
+    const int rows = M.rows;
+    static_assert(G::THREADS == 512, "k_resnet_w8 geometries");
     const unsigned grid = (unsigned)((rows + G::BOARDS - 1) / G::BOARDS);
-    constexpr auto kern = [] {
-        if constexpr (G::THREADS == 512) return &k_resnet_w8<G, DT, IN, ABL>;
-        else return &k_resnet<G, DT, IN, ABL>;
-    }();
+    constexpr auto kern = &k_resnet_w8<G, DT, IN>;
     static bool configured = false;
     if (!configured) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   G::LDS);
         configured = true;
     }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(G::THREADS), G::LDS, s, N, feat, fw, H, rows, pol, val);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(G::THREADS), G::LDS, s, N, feat, fw, H, M, pol, val);
 }
 
-#ifdef OAMD_ABLATION
-static int ablation() {
-    static int v = [] {
-        const char* e = getenv("OAMD_RESNET_ABLATE");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-#endif
-
-#ifndef OAMD_TWO_PER_CU
-#define OAMD_TWO_PER_CU 0
-#endif
-#ifndef OAMD_SMALL_BATCH_ROWS
-#define OAMD_SMALL_BATCH_ROWS 1024
-#endif
-constexpr int kSmallBatchRows = OAMD_SMALL_BATCH_ROWS;
+// Below kSmallBatchRows rows the throughput geometry would leave most CUs idle
+// and its per-workgroup latency (4 or 2 boards through the whole tower) sets
+// the call's latency: one board per workgroup instead. The K order and MFMA
+// tiling per output are the same, so results are bit-identical.
+constexpr int kSmallBatchRows = 1024;
 
 template <int IN>
-static void dispatch(const NetView& N, const void* feat, int fw, int H, int rows, float* pol,
-                     float* val, hipStream_t s) {
+static void dispatch(const NetView& N, const void* feat, int fw, int H, const RowMap& M, float* pol, float* val,
+                     hipStream_t s) {
+    const int rows = M.rows;
     if (rows <= 0) return;
-#ifdef OAMD_ABLATION
-    if constexpr (IN == kF32) {
-        if (N.C == 128 && N.dtype == OAMD_BF16 && ablation()) {
-            switch (ablation()) {
-                case 1: return launch_t<Geo<128>, OAMD_BF16, IN, 1>(N, feat, fw, H, rows, pol, val, s);
-                case 2: return launch_t<Geo<128>, OAMD_BF16, IN, 2>(N, feat, fw, H, rows, pol, val, s);
-                case 4: return launch_t<Geo<128>, OAMD_BF16, IN, 4>(N, feat, fw, H, rows, pol, val, s);
-                case 6: return launch_t<Geo<128>, OAMD_BF16, IN, 6>(N, feat, fw, H, rows, pol, val, s);
-                case 8: return launch_t<Geo<128>, OAMD_BF16, IN, 8>(N, feat, fw, H, rows, pol, val, s);
-                case 9: return launch_t<Geo<128>, OAMD_BF16, IN, 9>(N, feat, fw, H, rows, pol, val, s);
-                case 15: return launch_t<Geo<128>, OAMD_BF16, IN, 15>(N, feat, fw, H, rows, pol, val, s);
-                case 16: return launch_t<Geo<128>, OAMD_BF16, IN, 16>(N, feat, fw, H, rows, pol, val, s);
-                case 32: return launch_t<Geo<128>, OAMD_BF16, IN, 32>(N, feat, fw, H, rows, pol, val, s);
-                default: break;
-            }
-        }
-    }
-#endif
-    // Below kSmallBatchRows rows the throughput geometry would leave most CUs
-    // idle and its per-workgroup latency (4 or 2 boards through the whole tower)
-    // sets the call's latency: one board per workgroup instead. The K order and
-    // MFMA tiling per output are the same, so results are bit-identical.
     const bool small = rows < kSmallBatchRows;
+    const bool fp16 = N.dtype == OAMD_FP16;
     if (N.C == 128) {
         if (small) {
-            if (N.dtype == OAMD_FP16) launch_t<GeoS<128>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
-            else launch_t<GeoS<128>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+            if (fp16) launch_t<GeoS<128>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s);
+            else launch_t<GeoS<128>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s);
         } else {
-#if OAMD_TWO_PER_CU
-            if (N.dtype == OAMD_FP16) launch_t<Geo2<128>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
-            else launch_t<Geo2<128>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
-#else
-            if (N.dtype == OAMD_FP16) launch_t<Geo<128>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
-            else launch_t<Geo<128>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
-#endif
+            if (fp16) launch_t<Geo<128>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s);
+            else launch_t<Geo<128>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s);
         }
     } else {
         if (small) {
-            if (N.dtype == OAMD_FP16) launch_t<GeoS<256>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
-            else launch_t<GeoS<256>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+            if (fp16) launch_t<GeoS<256>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s);
+            else launch_t<GeoS<256>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s);
         } else {
-            if (N.dtype == OAMD_FP16) launch_t<Geo<256>, OAMD_FP16, IN>(N, feat, fw, H, rows, pol, val, s);
-            else launch_t<Geo<256>, OAMD_BF16, IN>(N, feat, fw, H, rows, pol, val, s);
+            if (fp16) launch_t<Geo<256>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s);
+            else launch_t<Geo<256>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s);
         }
     }
 }
 
 void launch_resnet_packed(const NetView& N, const uint64_t* feat, int fw, int H, int rows,
-                          float* policy, float* value, hipStream_t s) {
-    dispatch<kPacked>(N, feat, fw, H, rows, policy, value, s);
+                          float* policy, float* value, hipStream_t s, const int32_t* rowlist,
+                          const int32_t* rowcount, int list_off) {
+    dispatch<kPacked>(N, feat, fw, H, RowMap{rowlist, rowcount, list_off, rows}, policy, value, s);
 }
 
 void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* policy, float* value,
                        hipStream_t s) {
-    dispatch<kF32>(N, feat, 0, 0, rows, policy, value, s);
+    dispatch<kF32>(N, feat, 0, 0, RowMap{nullptr, nullptr, 0, rows}, policy, value, s);
 }
 
 int resnet_read_stamps(unsigned long long* out, long long n) {

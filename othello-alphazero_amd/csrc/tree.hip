@@ -187,13 +187,31 @@ __device__ __forceinline__ void write_packed_features(const EngineView& E, size_
     }
 }
 
+// Append the NN rows of non-terminal leaves among rows c0 + j (bit j of
+// `valid`) to the group's evaluation list: one atomic per chunk of <= 64 rows
+// reserves the slots, lane j writes row c0 + j. The ResNet launch reads the
+// list, so terminal leaves cost it nothing (the reference builds no NN row for
+// them, search_thread.cpp:88-90); the list order does not matter, every row's
+// evaluation is independent of its place in a launch.
+__device__ __forceinline__ void append_rows(const EngineView& E, int* cnt, int list_base, int c0, uint64_t valid) {
+    const int n = popcount64(valid);
+    if (n == 0) return;
+    int slot = 0;
+    if (lane_id() == 0) slot = atomicAdd(cnt, n);
+    slot = readlane_i(slot, 0);
+    const int lane = lane_id();
+    if ((valid >> lane) & 1ULL)
+        E.rowlist[list_base + slot + popcount64(valid & ((1ULL << lane) - 1ULL))] = c0 + lane;
+}
+
 // ---------------------------------------------------------------------------
 // Selection: descents i in [i0, i1) with virtual loss (search_thread.cpp:59-100).
+// cnt != nullptr: the non-terminal leaves' rows go to the evaluation list.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void select_range(const EngineView& E, int g, GameState* gs, size_t base,
                                              int i0, int i1, uint64_t& event, int hist_node,
                                              int hist_n, unsigned long long& sims,
-                                             unsigned long long& evals) {
+                                             unsigned long long& evals, int* cnt, int list_base) {
     const int lane = lane_id();
     const int root = gs->root;
     const uint64_t key = gs->key;
@@ -202,6 +220,8 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
     // selected leaf (search_thread.cpp:78)
     const NodeLink root_link = load_link(E.link + base + root);
     int root_n = E.stat[base + root].n;
+    uint64_t valid_rows = 0;  // bit i - c0: row i is an NN row (chunks of 64 rows from i0)
+    int c0 = i0;
 
     for (int i = i0; i < i1; ++i) {
         const int r = g * E.L + i;
@@ -298,6 +318,14 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
         write_packed_features(E, base, r, d, p0, p1, hist_node, hist_n, lk.player, t, valid);
         sims += 1;
         evals += valid ? 1 : 0;
+        if (cnt) {
+            valid_rows |= (uint64_t)(valid ? 1 : 0) << (i - c0);
+            if (i - c0 == 63 || i == i1 - 1) {
+                append_rows(E, cnt, list_base, g * E.L + c0, valid_rows);
+                valid_rows = 0;
+                c0 = i + 1;
+            }
+        }
         wait_stores();  // the next descent reads these statistics
     }
 }
@@ -445,10 +473,15 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
 // k_resnet_w8 waves of every SIMD (512 VGPRs): one pipeline group's tree round
 // runs on the CUs that the other group's ResNet launch occupies. The cap costs
 // two 8-byte spills outside the descent/backup loops.
+// Evaluation list (cnt_add != nullptr, the native search): the rows of
+// non-terminal leaves this round selects are appended to E.rowlist[g0 * L ..]
+// behind the counter *cnt_add; *cnt_reset (the counter of the next round,
+// which no launch still reads) is zeroed by the group's first wave.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree(EngineView E, int g0, int do_backup, int do_select,
-                                             int t0, int t1, int B) {
+                                             int t0, int t1, int B, int* cnt_add, int* cnt_reset) {
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
+    if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
     GameState* gs = E.games + g;
     const size_t base = (size_t)g * E.cap;
     const int flags = gs->flags;
@@ -474,7 +507,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     bool overflow = false;
     for (int t = t0; t < t1; ++t) {
         if (do_backup) backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
-        if (do_select) select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals);
+        if (do_select)
+            select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals, cnt_add,
+                         g0 * E.L);
     }
     if (lane == 0) {
         gs->event = event;
@@ -883,12 +918,13 @@ __global__ void k_apply_positions(const Pos* in, const int32_t* actions, Pos* ou
 static inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
-                 int g0, int ng, int t0, int t1) {
+                 int g0, int ng, int t0, int t1, int* cnt_add, int* cnt_reset) {
     if (ng < 0) ng = E.G - g0;
     if (t1 < 0) t1 = T;
     if (T * B != E.L || t0 < 0 || t1 > T || t0 >= t1) return;  // caller validated; never launch on a mismatched layout
     if (ng > 0 && (do_backup || do_select))
-        hipLaunchKernelGGL(k_tree, dim3(ng), dim3(64), 0, s, E, g0, (int)do_backup, (int)do_select, t0, t1, B);
+        hipLaunchKernelGGL(k_tree, dim3(ng), dim3(64), 0, s, E, g0, (int)do_backup, (int)do_select, t0, t1, B,
+                           do_select ? cnt_add : nullptr, cnt_reset);
 }
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s) {
     if (rows > 0) hipLaunchKernelGGL(k_features_f32, dim3(blocks_for(rows, 4)), dim3(256), 0, s, E, out, row_begin, rows);

@@ -201,10 +201,10 @@ def test_resnet_activation_layout_is_bank_conflict_free():
             for m in range(4):
                 assert conflict_free(C, [b * stride(C) + pad_row(tile[m][j]) for j in range(16)])
 
-    # edge-row tiling (OAMD_EDGE, edge_tile_row): tile m of position group q is
-    # board row y = 4h + m of boards P and P + NPAIR. 64-position waves (PW 64,
-    # the OAMD_WIDE=0 alternative): SIMD partners (q, q + NPAIR) own rows 0-3 /
-    # 4-7; 128-position waves (PW 128, OAMD_WIDE, the default): rows 0-7
+    # edge-row tiling (edge_tile_row): tile m of position group q is board row
+    # y = 4h + m of boards P and P + NPAIR; the kernel's 128-position waves (PW
+    # 128) own rows 0-7 of their pair (64-position waves, rows 0-3 / 4-7 of a
+    # half, are checked too: the layout serves both)
     def edge_tile_row(C, q, m, j):
         npair = 512 // C // 2
         P, h = q % npair, q // npair
@@ -234,7 +234,7 @@ def test_resnet_activation_layout_is_bank_conflict_free():
 
 
 def test_resnet_wide_order_window_and_skips():
-    """The default tower order of csrc/resnet.hip (OAMD_WIDE: wide_cb, wide_dy,
+    """The tower order of csrc/resnet.hip (wide_cb, wide_dy,
     wide_new; resnet_kstep): per dx and 32-channel block the K-steps dy = -1,
     0, +1. Every (tap, block) once per layer; 128-position waves own rows 0-7,
     so every wave leaves out tile 0 at dy = -1 (row -1) and tile 7 at dy = +1
@@ -262,44 +262,6 @@ def test_resnet_wide_order_window_and_skips():
             skipped = set(range(8)) - set(tiles)
             assert all(m + dy(J) in (-1, 8) for m in skipped)  # border rows only
         assert all(h == set(range(1, 9)) for h in held.values())
-
-
-def test_resnet_sweep_order_window_and_skips():
-    """Restates the tower's dy-sweep K order of csrc/resnet.hip (sweep_cb,
-    sweep_dy, sweep_new; resnet_kstep for C=128) and checks what the kernel
-    relies on: every (tap, 32-channel block) once per layer; each 2-K-step
-    weight stage is either (dy -1, dy +1) of one block, where waves 0-3 skip
-    tile 0 and waves 4-7 tile 3 (one skip each: balanced barriers), or the
-    dy = 0 K-steps of two blocks; and the register window (row i = board row i - 1 of the
-    half) holds every row a K-step reads, each row read once per block and dx
-    and before its first use."""
-    def cb(J):
-        return J // 3
-
-    def dy(J):
-        return -1 if J % 6 in (0, 4) else (1 if J % 6 in (1, 5) else 0)
-
-    new = {0: 0x0F, 1: 0x30, 2: 0, 3: 0x1E, 4: 0x01, 5: 0x20}
-    for nb in (4, 8):  # C = 128, 256: every (tap, block) once per layer
-        seq = [(dxi + 3 * (dy(J) + 1), cb(J)) for dxi in range(3) for J in range(3 * nb)]
-        assert sorted(seq) == [(t, c) for t in range(9) for c in range(nb)]
-    for dxi in range(3):
-        for st in range(6):
-            a, b = 2 * st, 2 * st + 1
-            assert (dy(a), dy(b)) in ((-1, 1), (0, 0))
-            assert dy(a) == 0 or cb(a) == cb(b)
-        held = {}
-        for J in range(12):
-            c = cb(J)
-            loaded = {i for i in range(6) if (new[J % 6] >> i) & 1}
-            assert not (loaded & held.get(c, set()))  # read once per block and dx
-            held.setdefault(c, set()).update(loaded)
-            need = {m + 1 + dy(J) for m in range(4)}
-            assert need <= held[c]
-        assert all(h == set(range(6)) for h in held.values())
-    # the skipped tiles lie on the border: top half tile 0 (row 0) at dy = -1
-    # reads row -1, bottom half tile 3 (row 7) at dy = +1 reads row 8
-    assert 0 + (-1) == -1 and (4 + 3) + 1 == 8
 
 
 def test_type_stub_covers_the_reference_surface_and_the_module():

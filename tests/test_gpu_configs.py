@@ -113,3 +113,113 @@ def test_configs4_shard(om):
         runs.append((v.cpu(), q.cpu()))
     assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
     numerics.record("configs[4] shard", "512 games fp16: eval batch 2048 == whole-group launches")
+
+
+def test_configs1_tree_vs_oracle_full_shape(om):
+    """configs[1]'s tree at full shape against the oracle:
+    256 games, H=8, T=2 x B=16, 800 sims, eps=0.25 (Dirichlet noise from each
+    game's random stream), 8192-row k_tree rounds through the step API with
+    the equivariant stub, 2 moves with tree reuse after 0-8
+    random opening plies. A fixed subset of 64 games is replayed by
+    OracleMCTS(game_key=...) (oracle/omcts_oracle.c, pinned by the compiled
+    reference's fixtures): visit counts, Q bits and the 8-fold self_play_data
+    per move. The native search at this shape equals this callback search
+    (test_configs1_full_shape), which closes the chain for the bench path.
+    Reference: search_thread.cpp:59-260, mcts.cpp:45-165."""
+    import oracle as O
+
+    G, H, L = 256, 8, 32
+    b = om.BatchedMCTS(G, history_size=H, num_simulations=800, num_threads=2, batch_size=16,
+                       dirichlet_epsilon=0.25, seed=303)
+    rng = np.random.default_rng(404)
+    subset = sorted(rng.choice(G, 64, replace=False).tolist())
+    refs = {g: O.OracleMCTS(history_size=H, num_simulations=800, num_threads=2, batch_size=16,
+                            dirichlet_epsilon=0.25, game_key=b.engine.game_key(g)) for g in subset}
+    # random openings from the host, applied to the engine and to the oracles
+    plies = rng.integers(0, 9, G)
+    for k in range(int(plies.max())):
+        acts = torch.full((G,), -1, dtype=torch.int32)
+        for g in range(G):
+            if k < plies[g]:
+                legal = O.legal_actions(_pos(b, g))
+                acts[g] = int(legal[rng.integers(len(legal))])
+                if g in refs:
+                    refs[g].apply_action(int(acts[g]))
+        b.apply_actions(acts.to(DEV))
+
+    def stub(features):
+        p, v = O.equivariant_stub(features.cpu().numpy())
+        return {"policy": torch.from_numpy(p), "value": torch.from_numpy(v)}
+
+    for mv in range(2):
+        sims, evals = b.search(stub)
+        assert sims == G * 800 and 0 < evals <= sims
+        acts = torch.full((G,), -1, dtype=torch.int32)
+        for g, r in refs.items():
+            r.search(O.equivariant_stub)
+            info = b.root_info(g)
+            assert info["visit_counts"] == r.visit_counts(), (mv, g)
+            np.testing.assert_array_equal(np.array(info["mean_action_values"], np.float32),
+                                          np.array(r.mean_action_values(), np.float32))
+            d = b.self_play_data(g)
+            f, p = r.self_play_data()
+            np.testing.assert_array_equal(torch.stack(d["features"]).numpy(), f)
+            np.testing.assert_array_equal(torch.stack(d["policy"]).numpy(), p)
+            vc = r.visit_counts()
+            acts[g] = O.legal_actions(r.position())[int(np.argmax(vc))]
+            r.apply_action(int(acts[g]))
+        v, _ = b.root_stats()
+        for g in range(G):  # the other games move too (argmax of their visits)
+            if g not in refs:
+                row = v[g].cpu().numpy()
+                acts[g] = int(np.argmax(row)) if row.max() > 0 else -1
+        b.apply_actions(acts.to(DEV))
+    assert b.engine.status() == (0, 0)
+    numerics.record("configs[1] tree vs oracle", f"G={G}, 64 games replayed by the oracle: 2 moves, visits, Q bits, "
+                                                 "8-fold targets identical")
+
+
+def _pos(b, g):
+    import oracle as O
+
+    i = b.root_info(g)
+    return O.CPos(i["player"], i["player1_discs"], i["player2_discs"], i["legal_moves"], i["next_legal_moves"])
+
+
+def test_evaluation_lists_through_endgames(om):
+    """The native search evaluates only the rows of non-terminal leaves (the
+    per-group evaluation lists of tree.hip append_rows, read by the ResNet
+    launch): through whole games, restarts and endgames full of terminal
+    leaves it must give every game the same visits and Q as the callback path,
+    which evaluates every row. 64 games = 2 pipeline groups of 1024-row
+    throughput launches; eval batch 384 splits them at list offsets."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(41, 9, 128, 1, 32), device=0)
+    kw = dict(history_size=4, num_simulations=64, num_threads=2, batch_size=16, dirichlet_epsilon=0.25, seed=5,
+              node_capacity=1 << 16)
+    a, c, e = om.BatchedMCTS(64, **kw), om.BatchedMCTS(64, **kw), om.BatchedMCTS(64, **kw)
+    e.engine.set_nn_batch(384)
+    for x in (a, c, e):
+        x.random_openings(8, seed=6)
+    total_sims = total_evals = 0
+    for mv in range(75):
+        sa, ea = a.search(net)
+        sc, ec = c.search(lambda f: net(f))
+        se, ee = e.search(net)
+        assert (sa, ea) == (sc, ec) == (se, ee), mv
+        total_sims += sa
+        total_evals += ea
+        va, qa = a.root_stats()
+        vc, qc = c.root_stats()
+        ve, qe = e.root_stats()
+        assert torch.equal(va, vc) and torch.equal(qa, qc), mv
+        assert torch.equal(va, ve) and torch.equal(qa, qe), mv
+        xa = a.selfplay_move(temperature_moves=12, opening_moves=4)["actions"]
+        xc = c.selfplay_move(temperature_moves=12, opening_moves=4)["actions"]
+        xe = e.selfplay_move(temperature_moves=12, opening_moves=4)["actions"]
+        assert torch.equal(xa, xc) and torch.equal(xa, xe), mv
+    share = 1.0 - total_evals / total_sims
+    numerics.record("evaluation lists", f"64 games x 75 moves: terminal-leaf share {share:.3f}, "
+                                        "native (lists, eval batch 0 / 384) == callback")
+    assert share > 0.02  # the endgames were reached

@@ -33,11 +33,6 @@ step() {  # step LIMIT LOG cmd...
   return $rc
 }
 
-with_vars() {  # with_vars "A=1 B=2" cmd...: env assignments then the command
-  local vars=$1; shift
-  env $vars "$@"
-}
-
 restore_lib() { [ -f /tmp/liboamd.so.orig ] && cp /tmp/liboamd.so.orig $PKG/liboamd.so; }
 
 run_recipe() {
@@ -52,9 +47,9 @@ run_recipe() {
     pmc) local n=$1 c=$2; shift 2
       step 300 "$OUT/pmc_$n.log" rocprofv3 --pmc ${c//,/ } --kernel-trace -T -d "$OUT/pmc_$n" -o run \
         --output-format csv -- python3 bench.py "$@" ;;
-    nn) local n=$1; shift; step 300 "$OUT/nn_$n.log" with_vars "$*" python tools/nn_kernel.py ;;
+    nn) local n=$1; shift; step 300 "$OUT/nn_$n.log" env "$@" python tools/nn_kernel.py ;;
     nnpmc) local n=$1 c=$2; shift 2
-      step 300 "$OUT/nnpmc_$n.log" with_vars "$*" rocprofv3 --pmc ${c//,/ } --kernel-trace -d "$OUT/nnpmc_$n" \
+      step 300 "$OUT/nnpmc_$n.log" env "$@" rocprofv3 --pmc ${c//,/ } --kernel-trace -d "$OUT/nnpmc_$n" \
         -o run --output-format csv -- python3 tools/nn_kernel.py ;;
     latency) step 600 "$OUT/latency_$1.log" python tools/latency.py ;;
     variants) local n=$1; shift
@@ -63,7 +58,7 @@ run_recipe() {
       for r in $(seq ${ROUNDS:-2}); do
         for v in ${AB_ORDER:-$(ls abv)}; do
           cp abv/$v/liboamd.so $PKG/liboamd.so
-          step 300 "$OUT/var_${n}_${v}_$r.log" with_vars "AB_REF=$ref $*" python tools/nn_kernel.py || { restore_lib; return 1; }
+          step 300 "$OUT/var_${n}_${v}_$r.log" env AB_REF=$ref "$@" python tools/nn_kernel.py || { restore_lib; return 1; }
         done
       done
       restore_lib ;;
