@@ -193,7 +193,10 @@ int oamd_debug_read_stamps(uint64_t *out, int64_t n);
  * Calling backup after every select gives the lock-step order instead. */
 int oamd_engine_search_begin(oamd_engine *e, int32_t *steps);
 int oamd_engine_select(oamd_engine *e);
-/* host_out[row] = 1 when the leaf is non-terminal (needs the NN) */
+/* host_out[row] = 1 when the row needs the NN this round: a non-terminal leaf
+ * of a batch that waits for its evaluation (a virtual thread whose batch was
+ * all terminal backed it up without one and selected again,
+ * search_thread.cpp:102-127; a thread that ran out of batches has none) */
 int oamd_engine_leaf_flags(oamd_engine *e, uint8_t *host_out);
 /* features_dev: (rows, 1 + 2H, 8, 8) fp32 of rows [row_begin, row_begin+rows) */
 int oamd_engine_features(oamd_engine *e, float *features_dev, int32_t row_begin, int32_t rows);

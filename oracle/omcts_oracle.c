@@ -534,6 +534,36 @@ static void evaluate_thread(orc_mcts *m, int th, orc_nn_fn nn, void *user) {
            m->value + (size_t)th * B);
 }
 
+static int batch_any_live(const orc_mcts *m, int th) {
+    for (int j = 0; j < m->batch_size; ++j)
+        if (m->nodes[m->leaves[th * m->batch_size + j]].pos.player != 0) return 1;
+    return 0;
+}
+
+static void backup_thread(orc_mcts *m, int th) {
+    for (int j = 0; j < m->batch_size; ++j) {
+        int i = th * m->batch_size + j;
+        expand_and_backward(m, m->leaves[i], m->trans[i], m->policy + (size_t)i * 65, m->value + i);
+    }
+}
+
+/* Thread th selects its next batches (search_thread.cpp:60-81) until one has
+ * a non-terminal leaf, which then waits for the NN; a batch whose leaves are
+ * all terminal needs no NN round trip (:102) and is backed up at once
+ * (:116-127) before the thread selects again. At most `steps` batches per
+ * thread and search (:47-57). */
+static void select_thread(orc_mcts *m, int th, int steps, int *sel, int *pend) {
+    while (sel[th] < steps) {
+        for (int j = 0; j < m->batch_size; ++j) select_leaf(m, th * m->batch_size + j);
+        ++sel[th];
+        if (batch_any_live(m, th)) {
+            pend[th] = 1;
+            return;
+        }
+        backup_thread(m, th);
+    }
+}
+
 /* Schedule of the reference's T threads x B leaves (search_thread.cpp:47-128,
  * mcts.h:220-256). Each thread runs ceil(S / (T*B)) batches of
  * lock{select B} -> NN round trip -> lock{expand + backup B}; the calling
@@ -546,23 +576,30 @@ static void evaluate_thread(orc_mcts *m, int th, orc_nn_fn nn, void *user) {
  *
  * (S = select a batch, B = back it up): a thread whose NN result arrives
  * backs up and immediately selects its next batch while the NN serves the
- * next thread. With T = 1 this is exactly the reference's sequential loop. */
+ * next thread; a thread whose selected batch is all terminal skips the NN and
+ * backs up and selects again right away (select_thread), so near the end of a
+ * game threads run ahead of each other. With T = 1 this is exactly the
+ * reference's sequential loop. */
 int orc_mcts_search(orc_mcts *m, orc_nn_fn nn, void *user) {
     int T = m->num_threads, B = m->batch_size, L = T * B;
     int steps = (m->num_simulations + L - 1) / L;
-    for (int round = 0; round <= steps; ++round) {
-        for (int th = 0; th < T; ++th) {
-            if (round > 0)
-                for (int j = 0; j < B; ++j) {
-                    int i = th * B + j;
-                    expand_and_backward(m, m->leaves[i], m->trans[i], m->policy + (size_t)i * 65,
-                                        m->value + i);
-                }
-            if (round < steps)
-                for (int j = 0; j < B; ++j) select_leaf(m, th * B + j);
-        }
-        if (round < steps)
-            for (int th = 0; th < T; ++th) evaluate_thread(m, th, nn, user);
+    int sel[1024], pend[1024];
+    for (int t = 0; t < T; ++t) sel[t] = pend[t] = 0;
+    for (int t = 0; t < T; ++t) select_thread(m, t, steps, sel, pend);
+    for (;;) {
+        int any = 0;
+        for (int t = 0; t < T; ++t)
+            if (pend[t]) {
+                any = 1;
+                evaluate_thread(m, t, nn, user);
+            }
+        if (!any) break;
+        for (int t = 0; t < T; ++t)
+            if (pend[t]) {
+                backup_thread(m, t);
+                pend[t] = 0;
+                select_thread(m, t, steps, sel, pend);
+            }
     }
     return steps * L;
 }

@@ -150,6 +150,7 @@ struct oamd_engine {
     // round being evaluated, the next round's)
     int32_t* rowlist = nullptr;
     int32_t* rowcount = nullptr;
+    int32_t* tstate = nullptr;  // per game and virtual thread: batches selected, pending (k_tree)
     float* explore_tab = nullptr;
     unsigned long long* counters = nullptr;
     int32_t* status_dev = nullptr;  // [0] games with pool overflow, [1] depth-capped games
@@ -288,6 +289,9 @@ struct oamd_engine {
         E.alpha = cfg.dirichlet_alpha;
         E.counters = counters;
         E.rowlist = rowlist;
+        E.tstate = tstate;
+        E.steps = (cfg.num_simulations + L() - 1) / L();
+        E.B = cfg.batch_size;
         return E;
     }
 
@@ -304,11 +308,12 @@ struct oamd_engine {
         dfree(value);
         dfree(flags);
         dfree(rowlist);
+        dfree(tstate);
         int rc;
         if ((rc = dalloc(&leaf, rows)) || (rc = dalloc(&depth, rows)) || (rc = dalloc(&trans, rows)) ||
             (rc = dalloc(&path, rows * kMaxDepth)) || (rc = dalloc(&feat, rows * fw)) ||
             (rc = dalloc(&policy, rows * 65)) || (rc = dalloc(&value, rows)) || (rc = dalloc(&flags, rows)) ||
-            (rc = dalloc(&rowlist, rows)))
+            (rc = dalloc(&rowlist, rows)) || (rc = dalloc(&tstate, rows)))
             return rc;
         HIPCHK(hipMemset(policy, 0, rows * 65 * sizeof(float)));
         HIPCHK(hipMemset(value, 0, rows * sizeof(float)));
@@ -342,6 +347,7 @@ struct oamd_engine {
         dfree(value);
         dfree(flags);
         dfree(rowlist);
+        dfree(tstate);
         dfree(rowcount);
         dfree(explore_tab);
         dfree(counters);
@@ -482,7 +488,7 @@ int oamd_net_create(int32_t device, const oamd_net_desc* d, oamd_net** out) {
     net->desc = *d;
     const int C = d->conv_channels, R = d->num_residual_blocks, hid = d->value_head_hidden_channels;
     int rc;
-    if ((rc = dalloc(&net->w, resnet_packed_weight_elems(C, R))) ||
+    if ((rc = dalloc(&net->w, resnet_packed_weight_alloc_elems(C, R))) ||
         (rc = dalloc(&net->bias, (size_t)(1 + 2 * R) * C)) ||
         (rc = dalloc(&net->head, resnet_head_floats(C, hid))) ||
         (rc = dalloc(&net->hconv, resnet_hconv_elems(C)))) {
@@ -573,7 +579,7 @@ int oamd_net_load_state(oamd_net* net, const float* const* t, int32_t n_tensors)
     size_t ks_global = 0;
     // fold BN into a 3x3 conv and pack in MFMA A-fragment order, K-step by K-step
     // (resnet_kstep): [ks][ntile][lane][8]; lane holds output channel
-    // ntile*16 + (lane&15) and input channels cb*32 + 8*chunk(lane>>4) + j
+    // resnet_out_channel(ntile, lane&15) and input channels cb*32 + 8*chunk(lane>>4) + j
     auto pack_conv = [&](int layer, int cin, bool first) {
         const float* W = t[ti++];
         const float* b = t[ti++];
@@ -596,7 +602,7 @@ int oamd_net_load_state(oamd_net* net, const float* const* t, int32_t n_tensors)
                 for (int lane = 0; lane < 64; ++lane)
                     for (int j = 0; j < 8; ++j) {
                         const int ci = cb * 32 + 8 * resnet_kgroup_chunk(lane >> 4) + j;
-                        const int n = nt * 16 + (lane & 15);
+                        const int n = resnet_out_channel(nt, lane & 15);
                         double v = 0.0;
                         if (!pad && ci < cin) v = (double)W[((size_t)n * cin + ci) * 9 + tap] * scale[n];
                         const size_t idx = (((ks * (C / 16) + nt) * 64) + lane) * 8 + j;
@@ -673,6 +679,8 @@ int oamd_net_load_state(oamd_net* net, const float* const* t, int32_t n_tensors)
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(net->hconv, hconv.data(), hconv.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(net->w, packed.data(), packed.size() * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(net->w + packed.size(), 0,
+                     (resnet_packed_weight_alloc_elems(C, R) - packed.size()) * sizeof(uint16_t)));
     HIPCHK(hipMemcpy(net->bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(net->head, head.data(), head.size() * 4, hipMemcpyHostToDevice));
     net->loaded = true;

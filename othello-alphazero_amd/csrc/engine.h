@@ -71,6 +71,9 @@ struct EngineView {
     float c_base, c_init, eps, alpha;
     unsigned long long* counters;  // [0] sims, [1] evals (this search), [2] sims, [3] evals (cumulative)
     int32_t* rowlist;  // G*L: evaluation lists (pipeline group k: from its first game's row)
+    int32_t* tstate;   // G*L (entry g*L + t for virtual thread t): batches selected | pending << 16
+    int32_t steps;     // batches per virtual thread and search: ceil(num_simulations / L)
+    int32_t B;         // batch_size (leaves per virtual thread and batch)
 };
 
 }  // namespace oamd

@@ -71,6 +71,7 @@ void launch_resnet_packed(const NetView& N, const uint64_t* feat, int fw, int H,
 void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* policy, float* value,
                        hipStream_t s);
 size_t resnet_packed_weight_elems(int C, int R);
+size_t resnet_packed_weight_alloc_elems(int C, int R);  // + the zero pad the stream may run into
 size_t resnet_head_floats(int C, int hidden);
 // elements of the packed 1x1 head-conv fragments (NetView::hconv)
 inline size_t resnet_hconv_elems(int C) { return (size_t)(C / 32) * 64 * 8; }
@@ -84,5 +85,7 @@ int resnet_ksteps(int C, bool first);
 void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad);
 // 8-channel chunk (0..3 within a K-step) that MFMA k-group kg (= lane >> 4) reads
 int resnet_kgroup_chunk(int kg);
+// output channel of row `row` (0..15) of MFMA output-channel tile `tile` (weights packing)
+int resnet_out_channel(int tile, int row);
 
 }  // namespace oamd

@@ -15,8 +15,8 @@
 //   * K is walked in K-steps of one tap x 32 input channels. Weights (BatchNorm
 //     folded, packed on the host in fragment order) stream once per workgroup
 //     through a 3-slot LDS ring by LDS-DMA (global_load_lds_dwordx4); a 16 KiB
-//     slot holds one stage = 256/C K-steps. The slot for stage g+2 is issued at
-//     the barrier that opens stage g+1, so fragment reads always overlap MFMAs;
+//     slot holds one stage = 256/C K-steps. Stage s+2 is issued at the barrier
+//     that opens stage s+1, so fragment reads always overlap MFMAs;
 //   * ONE activation buffer per workgroup, updated in place: each board is a
 //     zero-bordered 10x10 grid of rows of 2C+16 bytes ([position][channel]).
 //     The border makes every 3x3 tap read `lane base + uniform offset` (no
@@ -114,6 +114,16 @@ __host__ __device__ constexpr int ksteps_first(int C) {
 }
 __host__ __device__ constexpr int ksteps_tower(int C) { return 9 * (C / 32); }
 __host__ __device__ constexpr int kgroup_chunk(int kg) { return ((kg & 1) << 1) | (kg >> 1); }
+// Output channel computed by row 4 * kg + k of MFMA channel tile `tile` (an
+// accumulator lane of k-group kg holds rows 4 kg .. 4 kg + 3): the tiles 2j and
+// 2j + 1 of a 32-channel block interleave in groups of 4, so a lane's 8
+// accumulator channels of the pair are contiguous (channels 32j + 8kg .. +7)
+// and the epilogue stores them with one ds_write_b128. The host packs every
+// conv's weights and the kernel loads every bias in this order; activations
+// stay in plain channel order.
+__host__ __device__ constexpr int out_chan(int tile, int kg, int k) {
+    return 32 * (tile >> 1) + 8 * kg + 4 * (tile & 1) + k;
+}
 
 int resnet_ksteps(int C, bool first) { return first ? ksteps_first(C) : ksteps_tower(C); }
 void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad) {
@@ -129,9 +139,13 @@ void resnet_kstep(int C, bool first, int i, int* tap, int* cb, bool* pad) {
     }
 }
 int resnet_kgroup_chunk(int kg) { return kgroup_chunk(kg); }
+int resnet_out_channel(int tile, int row) { return out_chan(tile, row >> 2, row & 3); }
 size_t resnet_packed_weight_elems(int C, int R) {
     return (size_t)(ksteps_first(C) + 2 * R * ksteps_tower(C)) * 32 * C;
 }
+// + a zero pad of 4 stages: the weight stream runs up to AHEAD (<= 3) stages
+// past the last one (issue_stage_dma)
+size_t resnet_packed_weight_alloc_elems(int C, int R) { return resnet_packed_weight_elems(C, R) + 4 * kStageBytes / 2; }
 
 // ---- activation layout --------------------------------------------------------
 // padded row of board position p = 8y + x inside its board's 10x10 grid
@@ -370,14 +384,16 @@ __device__ __forceinline__ void mfma_frags(f32x4_t (&acc)[NT][MT], const Frags<N
         for (int m = 0; m < MT; ++m) acc[n][m] = mfma<DT>(f.w[n], f.x[m], acc[n][m]);
 }
 
-// Stages past the last one re-read the last stage into a slot nobody reads any
-// more: the issue stays branch-free and the vmcnt bookkeeping uniform.
-// PART: -1 = all of this wave's pieces of stage g; 0 / 1 = its first / second
-// piece (G::SPLIT_DMA).
+// LDS-DMA of the weight stage at `src` into ring slot `slot`. The stream
+// pointer advances by one stage per opening (a loop-carried scalar: the
+// compiler cannot hoist every stage's address to the top of a layer); stages
+// past the last one read the zero pad behind the packed weights
+// (resnet_packed_weight_alloc_elems) into a slot nobody reads any more, so
+// the issue stays branch-free and the vmcnt bookkeeping uniform.
+// PART: -1 = all of this wave's pieces of the stage; 0 / 1 = its first /
+// second piece (G::SPLIT_DMA).
 template <class G, int PART = -1>
-__device__ __forceinline__ void issue_stage_dma(const unsigned char* wsrc, unsigned char* ring, int g, int slot,
-                                                int total, int tid) {
-    const unsigned char* src = wsrc + (size_t)(g < total ? g : total - 1) * G::STAGE;
+__device__ __forceinline__ void issue_stage_dma(const unsigned char* src, unsigned char* ring, int slot, int tid) {
     unsigned char* dst = ring + slot * G::STAGE;
     const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
@@ -610,8 +626,7 @@ template <class G>
 __device__ __forceinline__ void load_bias(float4 (&bv)[G::NT], const NetView& N, int layer, int wn, int lane) {
 #pragma unroll
     for (int n = 0; n < G::NT; ++n)
-        bv[n] = *reinterpret_cast<const float4*>(N.bias + (size_t)layer * G::C + wn * G::WC + n * 16 +
-                                                 (lane >> 4) * 4);
+        bv[n] = *reinterpret_cast<const float4*>(N.bias + (size_t)layer * G::C + out_chan(wn * G::NT + n, lane >> 4, 0));
 }
 
 template <class G, int DT, int IN>
@@ -651,13 +666,13 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 #define OAMD_EP_MARK(k) ((void)0)
 #endif
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
-    const int total = (ksteps_first(C) + 2 * N.R * ksteps_tower(C)) / G::KS;
 
     // weight stream starts right away: stages 0 .. AHEAD (with SPLIT_DMA the
     // newest stage's second piece goes out at stage 0's second K-step)
 #pragma unroll
-    for (int s = 0; s < G::AHEAD; ++s) issue_stage_dma<G>(wsrc, ring, s, s, total, tid);
-    issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, G::AHEAD, G::AHEAD, total, tid);
+    for (int s = 0; s < G::AHEAD; ++s) issue_stage_dma<G>(wsrc + s * G::STAGE, ring, s, tid);
+    const unsigned char* wcur = wsrc + G::AHEAD * G::STAGE;  // the newest stage issued
+    issue_stage_dma<G, G::OPEN_PART>(wcur, ring, G::AHEAD, tid);
 
     float4 bv[kNT];  // folded bias of this lane's output channels (current layer)
     load_bias<G>(bv, N, 0, wn, lane);
@@ -671,7 +686,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                                   : wm * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) *
                          G::RP;
         rd[m] = rowb + kgroup_chunk(kg) * 16;
-        wr[m] = rowb + wn * G::WC * 2 + kg * 8;
+        wr[m] = rowb;
     }
     const int wl = (wn * kNT * 64 + lane) * 16;
 
@@ -750,8 +765,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     u32x4_t win0[kWide ? 9 : 1], win1[kWide ? 9 : 1];
     // window base: this lane's column, board row -1, dx = -1
     const int sb0 = rd[0] - 10 * G::RP - G::RP;
-    int g = 0;     // stage holding the current K-step
-    int slot = 0;  // g % RING
+    int slot = 0;  // ring slot of the stage holding the current K-step
 
     OAMD_STAMP(7);
     if constexpr (IN == kPacked) {
@@ -828,20 +842,21 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             // the barrier wait (+3.6 %)
             load_xfrags(nxt, act, xoff, rd);
             if constexpr (open) {
-                // open stage g+1: it has landed (this wave's DMAs, then everyone's
-                // via the barrier) and stage g-1's slot is drained by all waves
+                // open the next stage: it has landed (this wave's DMAs, then
+                // everyone's via the barrier), and the slot of the stage before the
+                // current one is drained by all waves: the newest stage goes there
                 wait_vm<G::VM_OPEN>();
                 __builtin_amdgcn_s_barrier();
                 const int sp = (slot + G::AHEAD + 1) % G::RING;  // (g + 1 + AHEAD) % RING
-                issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
-                ++g;
+                wcur += G::STAGE;
+                issue_stage_dma<G, G::OPEN_PART>(wcur, ring, sp, tid);
                 slot = slot == G::RING - 1 ? 0 : slot + 1;
             } else if constexpr (G::SPLIT_DMA) {
-                // the rest of stage g + AHEAD (its slot, stage g-1's, was freed
-                // by the barrier that opened stage g)
+                // the rest of the newest stage (its slot was freed by the barrier
+                // that opened the current stage)
                 int sa = slot + G::AHEAD;
                 sa = sa >= G::RING ? sa - G::RING : sa;
-                issue_stage_dma<G, G::MID_PART>(wsrc, ring, g + G::AHEAD, sa, total, tid);
+                issue_stage_dma<G, G::MID_PART>(wcur, ring, sa, tid);
             }
             constexpr int kis = open ? 0 : 1;  // K-step within its stage
             load_wfrags(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
@@ -912,13 +927,13 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     wait_vm<G::VM_OPEN>();
                     __builtin_amdgcn_s_barrier();
                     const int sp = (slot + G::AHEAD + 1) % G::RING;
-                    issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, sp, total, tid);
-                    ++g;
+                    wcur += G::STAGE;
+                    issue_stage_dma<G, G::OPEN_PART>(wcur, ring, sp, tid);
                     slot = slot == G::RING - 1 ? 0 : slot + 1;
                 } else if constexpr (G::SPLIT_DMA) {
                     int sa = slot + G::AHEAD;
                     sa = sa >= G::RING ? sa - G::RING : sa;
-                    issue_stage_dma<G, G::MID_PART>(wsrc, ring, g + G::AHEAD, sa, total, tid);
+                    issue_stage_dma<G, G::MID_PART>(wcur, ring, sa, tid);
                 }
                 load_wfrags(wn, ring + slot * G::STAGE + (open ? 0 : G::KSTEP_BYTES), wl);
 #pragma unroll
@@ -982,24 +997,41 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         const bool more = layer + 1 < nlayers;
         if (more) load_bias<G>(bv, N, layer + 1, wn, lane);
         OAMD_EP_MARK(0);
-        lds_barrier();  // every wave is done reading this layer's input and stage g
+        lds_barrier();  // every wave is done reading this layer's input and its last stage
         OAMD_EP_MARK(1);
-        issue_stage_dma<G, G::OPEN_PART>(wsrc, ring, g + 1 + G::AHEAD, (slot + G::AHEAD + 1) % G::RING, total,
-                                         tid);
-#pragma unroll
-        for (int n = 0; n < kNT; ++n)
+        wcur += G::STAGE;
+        issue_stage_dma<G, G::OPEN_PART>(wcur, ring, (slot + G::AHEAD + 1) % G::RING, tid);
+        if constexpr (kNT == 2) {
+            // the wave's two channel tiles hold 8 contiguous channels per lane
+            // (out_chan): one 16-byte store (and skip read) per position tile
+            const int co = 2 * out_chan(wn * 2, kg, 0);
 #pragma unroll
             for (int m = 0; m < kMT; ++m) {
-                u32x2_t* p = reinterpret_cast<u32x2_t*>(act + wr[m] + n * 32);
-                if constexpr (kind == 1) skip[n][m] = *p;  // block input, needed by conv2
-                const f32x4_t a = acc[n][m];
-                *p = u32x2_t{pack_relu<DT>(a[0], a[1]), pack_relu<DT>(a[2], a[3])};
+                u32x4_t* p = reinterpret_cast<u32x4_t*>(act + wr[m] + co);
+                if constexpr (kind == 1) {  // block input, needed by conv2
+                    const u32x4_t v = *p;
+                    skip[0][m] = u32x2_t{v.x, v.y};
+                    skip[1][m] = u32x2_t{v.z, v.w};
+                }
+                const f32x4_t a = acc[0][m], b = acc[1][m];
+                *p = u32x4_t{pack_relu<DT>(a[0], a[1]), pack_relu<DT>(a[2], a[3]), pack_relu<DT>(b[0], b[1]),
+                             pack_relu<DT>(b[2], b[3])};
             }
-        ++g;
+        } else {
+#pragma unroll
+            for (int n = 0; n < kNT; ++n)
+#pragma unroll
+                for (int m = 0; m < kMT; ++m) {
+                    u32x2_t* p = reinterpret_cast<u32x2_t*>(act + wr[m] + 2 * out_chan(wn * kNT + n, kg, 0));
+                    if constexpr (kind == 1) skip[n][m] = *p;  // block input, needed by conv2
+                    const f32x4_t a = acc[n][m];
+                    *p = u32x2_t{pack_relu<DT>(a[0], a[1]), pack_relu<DT>(a[2], a[3])};
+                }
+        }
         slot = slot == G::RING - 1 ? 0 : slot + 1;
         OAMD_EP_MARK(2);
         if (more) {
-            // stage g has landed (later may fly)
+            // the next layer's first stage has landed (later may fly)
             wait_vm<G::VM_LAYER>();
             lds_barrier();  // ... and this layer's output is complete
             if constexpr (kWide) {

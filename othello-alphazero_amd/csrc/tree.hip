@@ -506,10 +506,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     int count = gs->count;
     bool overflow = false;
     for (int t = t0; t < t1; ++t) {
-        if (do_backup) backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
-        if (do_select)
+        // virtual thread t: batches selected so far in this search, and whether
+        // its last batch waits for the NN (a search's first round starts fresh)
+        int* ts = E.tstate + (size_t)g * E.L + t;
+        const int st = do_backup ? *ts : 0;
+        int sel = st & 0xFFFF;
+        bool pend = (st >> 16) & 1;
+        if (do_backup && pend) {
+            backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
+            pend = false;
+        }
+        // the thread's next batch; one whose leaves are all terminal needs no NN
+        // round trip (search_thread.cpp:102) and is backed up at once (:116-127),
+        // then the thread selects again, up to `steps` batches per search
+        while (do_select && !pend && sel < E.steps) {
+            const unsigned long long ev0 = evals;
             select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals, cnt_add,
                          g0 * E.L);
+            ++sel;
+            if (evals != ev0) pend = true;
+            else backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
+        }
+        if (lane == 0) *ts = sel | (pend ? 1 << 16 : 0);
     }
     if (lane == 0) {
         gs->event = event;
@@ -560,9 +578,15 @@ __global__ __launch_bounds__(256) void k_set_evaluation(EngineView E, const floa
     if (idx < rows) E.value[row_begin + idx] = value[idx];
 }
 
+// 1 = the row is a non-terminal leaf of a batch that waits for the NN this
+// round (a thread that ran out of batches, or whose last batch was all
+// terminal, has none: its rows are stale)
 __global__ __launch_bounds__(256) void k_leaf_flags(EngineView E, uint8_t* flags) {
     const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r < E.G * E.L) flags[r] = (uint8_t)((E.feat[(size_t)r * E.FW] >> 16) & 1ULL);
+    if (r >= E.G * E.L) return;
+    const int g = r / E.L, t = (r % E.L) / E.B;
+    const bool pend = (E.tstate[(size_t)g * E.L + t] >> 16) & 1;
+    flags[r] = (uint8_t)(pend && ((E.feat[(size_t)r * E.FW] >> 16) & 1ULL));
 }
 
 // ---------------------------------------------------------------------------

@@ -90,23 +90,23 @@ class BatchedMCTS:
         # interleaving, csrc/tree.hip k_tree); one backup closes the search.
         rows = self.rows_per_step
         feat = torch.empty((rows, self._C, 8, 8), dtype=torch.float32, device=self.device)
+        sims0, evals0 = self.engine.work_counters()
         steps = self.engine.search_begin()
-        sims = evals = 0
         for _ in range(steps):
             self.engine.select()
-            # leaf flags: 1 = non-terminal leaf (an NN row); terminal leaves are
-            # simulations without an evaluation (search_thread.cpp:88-90)
-            flags = self.engine.leaf_flags()
+            # every row goes to the evaluator; rows of terminal leaves and of
+            # threads with no batch waiting this round are never read back
             self.engine.features(feat.data_ptr(), 0, rows)
             out = neural_net(feat)
             pol = out["policy"].detach().to(self.device, torch.float32).contiguous()
             val = out["value"].detach().to(self.device, torch.float32).contiguous()
             self.engine.set_evaluation(pol.data_ptr(), val.data_ptr(), 0, rows)
-            evals += int(flags.sum())
-            sims += rows  # every game of the engine is active (k_tree)
         self.engine.backup()
         self.engine.check_health()
-        return sims, evals
+        sims1, evals1 = self.engine.work_counters()
+        # simulations = leaf selections; evaluations = rows of non-terminal
+        # leaves (terminal ones need no NN, search_thread.cpp:88-90)
+        return sims1 - sims0, evals1 - evals0
 
     def check_health(self) -> None:
         """Raise RuntimeError if any game's node pool ran out or a descent hit

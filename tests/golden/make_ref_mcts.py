@@ -24,8 +24,10 @@ per-move features / policies, the value sequence, and the actions the
 reference's sampling rule chose (captured by a recording proxy around MCTS).
 
 Usage:  python tests/golden/make_ref_mcts.py        (after make -C oracle mcts)
+        python tests/golden/make_ref_mcts.py --endgame   (racy T=2 endgames only)
 Outputs (committed): tests/golden/ref_mcts.json, ref_mcts.npz,
-                     ref_self_play.json, ref_self_play.npz
+                     ref_self_play.json, ref_self_play.npz, ref_noise.*,
+                     ref_mcts_endgame.json (--endgame)
 Nothing from the reference (source, bytecode, binary) is copied into the repo.
 """
 
@@ -291,8 +293,47 @@ def make_noise_stats(om) -> None:
     np.savez_compressed(GOLD / "ref_noise.npz", **arrays)
 
 
+# ---------------------------------------------------------------- racy endgames
+def make_endgame_races(om, repeats: int = 20) -> None:
+    """Several search threads at the END of a game, where whole batches of
+    leaves are terminal. A thread whose batch is all terminal skips the NN
+    round trip and backs up and selects again at once (search_thread.cpp:
+    102-127), racing the other threads for the tree mutex, so repeated runs
+    of the reference rarely agree (recorded: the distinct trajectories and how
+    often each occurred). Every run's per-move visits and Q bits are stored,
+    and the tests require the HIP search's trajectory to be one the reference
+    produced. The last plies of the matrix's random game (through its pass),
+    T = 2."""
+    seed, acts, pass_ply = game_with_pass(om)
+    cases = []
+    for name, stub, H, B, S, n in (("eq_h4_t2_b8_s160_end", "equivariant", 4, 8, 160, 12),
+                                   ("eq_h4_t2_b16_s320_end", "equivariant", 4, 16, 320, 12),
+                                   ("uni_h4_t2_b8_s96_end", "uniform", 4, 8, 96, 10)):
+        case = {"name": name, "stub": stub, "history_size": H, "batch_size": B, "num_threads": 2,
+                "num_simulations": S, "dirichlet_epsilon": 0.0, "prefix": acts[:len(acts) - n],
+                "actions": acts[len(acts) - n:], "repeats": repeats}
+        runs = [_run_once(om, case) for _ in range(repeats)]
+        keys = [_key(r) for r in runs]
+        distinct = list(dict.fromkeys(keys))
+        case["trajectories"] = [{"count": keys.count(k),
+                                 "visits": [list(map(int, v)) for v in runs[keys.index(k)]["visits"]],
+                                 "q_bits": [[int(x) for x in q.view(np.uint32)] for q in runs[keys.index(k)]["q"]]}
+                                for k in distinct]
+        case["trajectories"].sort(key=lambda t: -t["count"])
+        cases.append(case)
+        print(f"{name}: {len(distinct)} distinct trajectories in {repeats} runs, "
+              f"counts {[t['count'] for t in case['trajectories']]}")
+    (GOLD / "ref_mcts_endgame.json").write_text(json.dumps({
+        "provenance": "compiled reference extension (oracle/Makefile target mcts), "
+                      "tests/golden/make_ref_mcts.py --endgame", "torch": torch.__version__,
+        "action_seed": seed, "cases": cases}, indent=0))
+
+
 if __name__ == "__main__":
     om = load_ref()
-    make_matrix(om)
-    make_self_play(om)
-    make_noise_stats(om)
+    if "--endgame" in sys.argv:
+        make_endgame_races(om)
+    else:
+        make_matrix(om)
+        make_self_play(om)
+        make_noise_stats(om)

@@ -116,3 +116,29 @@ def compare_visit_distributions(ours: np.ndarray, ref: np.ndarray) -> tuple[floa
     p = min(stats.ks_2samp(ours[:, j], ref[:, j]).pvalue for j in range(k)) * k
     ratio = max(abs(np.log(ours[:, j].std() / ref[:, j].std())) for j in range(k))
     return min(p, 1.0), float(np.exp(ratio))
+
+
+# ---------------------------------------------------------------- racy endgames
+def load_endgame_cases() -> list[dict]:
+    """tests/golden/ref_mcts_endgame.json: T = 2 searches over a game's last
+    plies, every distinct trajectory of 20 runs of the compiled reference."""
+    return json.loads((GOLD / "ref_mcts_endgame.json").read_text())["cases"]
+
+
+def endgame_trajectory(m, case: dict, search) -> tuple[list, list]:
+    """Per-move visit counts and Q bit patterns of `m` over the case."""
+    for a in case["prefix"]:
+        m.apply_action(a)
+    vis, qb = [], []
+    for a in case["actions"]:
+        search(m)
+        vis.append([int(v) for v in m.visit_counts()])
+        qb.append([int(x) for x in np.array(m.mean_action_values(), np.float32).view(np.uint32)])
+        m.apply_action(a)
+    return vis, qb
+
+
+def matching_runs(case: dict, vis: list, qb: list) -> int:
+    """How many of the reference's runs followed exactly this trajectory (0 =
+    none: the search is not one the reference produced)."""
+    return sum(t["count"] for t in case["trajectories"] if t["visits"] == vis and t["q_bits"] == qb)

@@ -219,6 +219,31 @@ def test_gpu_mcts_matches_reference_matrix(om, case):
     numerics.record(f"reference MCTS {case['name']}", f"moves={len(case['actions'])} q_ulp_flips={flips}")
 
 
+def _endgame_ids():
+    try:
+        return RF.load_endgame_cases()
+    except FileNotFoundError:  # pragma: no cover
+        return []
+
+
+@pytest.mark.parametrize("case", _endgame_ids(), ids=lambda c: c["name"])
+def test_gpu_endgame_races_reproduce_a_reference_run(om, case):
+    """The HIP search (drop-in MCTS, T = 2, k_tree's per-thread batch state) over
+    the last plies of a game, where whole batches are terminal and the
+    reference races (tests/golden/ref_mcts_endgame.json: 15-19 distinct
+    trajectories in 20 runs): its trajectory must be one the reference
+    produced, every move's visits and Q bits (search_thread.cpp:47-128)."""
+    m = _mcts(om, history_size=case["history_size"], num_simulations=case["num_simulations"],
+              num_threads=case["num_threads"], batch_size=case["batch_size"], dirichlet_epsilon=0.0)
+    stub = _torch_stub(O.equivariant_stub if case["stub"] == "equivariant" else O.uniform_stub)
+    vis, qb = RF.endgame_trajectory(m, case, lambda mm: mm.search(stub))
+    runs = RF.matching_runs(case, vis, qb)
+    numerics.record(f"reference endgame race {case['name']}",
+                    f"follows a trajectory {runs} of {case['repeats']} reference runs took "
+                    f"({len(case['trajectories'])} distinct)")
+    assert runs > 0
+
+
 @pytest.mark.parametrize("gi", [0, 1])
 def test_gpu_reproduces_reference_self_play(om, gi):
     """The reference's train._self_play game (compiled reference MCTS, np.random

@@ -269,3 +269,29 @@ def test_oracle_dirichlet_noise_distribution_matches_reference(idx):
         rows.append(m.visit_counts())
     p, r = RF.compare_visit_distributions(np.array(rows), ref)
     assert p > 1e-3 and r < 1.25, (st["name"], p, r)
+
+
+@pytest.mark.parametrize("case", RF.load_endgame_cases(), ids=lambda c: c["name"])
+def test_oracle_endgame_races_reproduce_a_reference_run(case):
+    """T = 2 over the last plies of a game, where threads' batches are all
+    terminal: the reference is racy there (15-19 distinct trajectories in 20
+    runs). The oracle's schedule (a thread with an all-terminal batch backs up
+    and selects again without the NN, search_thread.cpp:102-127) must follow
+    one of the recorded runs exactly, every move's visits and Q bits."""
+    m = O.OracleMCTS(history_size=case["history_size"], num_simulations=case["num_simulations"],
+                     num_threads=case["num_threads"], batch_size=case["batch_size"], dirichlet_epsilon=0.0,
+                     game_key=1)
+    stub = O.equivariant_stub if case["stub"] == "equivariant" else O.uniform_stub
+
+    class Adapter:  # the oracle's position() is a CPos, apply/search as the reference's
+        def apply_action(self, a):
+            m.apply_action(a)
+
+        def visit_counts(self):
+            return m.visit_counts()
+
+        def mean_action_values(self):
+            return m.mean_action_values()
+
+    vis, qb = RF.endgame_trajectory(Adapter(), case, lambda _: m.search(stub))
+    assert RF.matching_runs(case, vis, qb) > 0

@@ -1,26 +1,43 @@
 #!/bin/bash
-# Build liboamd.so variants of the ResNet kernel HERE (CPU container) for the
-# GPU-box recipes `variants` / `benchvar` of tools/gpu.sh:
-#   VARIANTS="name:extra flags[:path/to/resnet.hip];name2:..." bash tools/variants.sh
-# Each variant's resnet.hip (default: the tree's) is compiled with the build's
-# flags plus its extra ones and linked with the current tree/capi objects into
-# abv/<name>/liboamd.so. Build the default extension first (build.py).
+# Build liboamd.so variants HERE (CPU container) for the GPU-box recipes
+# `variants` / `benchvar` of tools/gpu.sh:
+#   VARIANTS="name:extra flags[:SRC];name2:..." bash tools/variants.sh
+# SRC: empty = the tree's resnet.hip with the tree's tree/capi objects;
+# a path = that resnet.hip with the tree's tree/capi objects; @REV = all of
+# csrc/ and include/ at git revision REV (capi.hip packs the weights, so a
+# variant that changes the packing must bring its own capi). Built into
+# abv/<name>/liboamd.so (the pybind layer binds the C ABI, not the variant).
 set -eu
 cd "$(dirname "$0")/.."
 B=othello-alphazero_amd/build
 CS=othello-alphazero_amd/csrc
 RF="-mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp"
+CXX="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -fno-gpu-rdc"
+EXACT="-ffp-contract=off -fno-fast-math"
 rm -rf abv
 IFS=';' read -ra SETS <<< "${VARIANTS:?}"
 pids=()
 for e in "${SETS[@]}"; do
   IFS=':' read -r name flags src <<< "$e"
-  src=${src:-$CS/resnet.hip}
   mkdir -p abv/$name
-  ( /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I $CS -I include -Wall -Wno-unused-function \
-      -fno-gpu-rdc $flags $RF -c $src -o abv/$name/resnet.o &&
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o abv/$name/liboamd.so abv/$name/resnet.o \
-      $B/tree.hip.o $B/capi.hip.o && rm abv/$name/resnet.o && echo "built $name" ) &
+  (
+    set -e
+    if [[ "${src:-}" == @* ]]; then
+      rev=${src#@}; d=abv/$name/src; mkdir -p $d
+      git archive "$rev" othello-alphazero_amd/csrc include | tar -x -C $d
+      inc="-I $d/$CS -I $d/include"
+      $CXX $inc $flags $RF -c $d/$CS/resnet.hip -o abv/$name/resnet.o
+      $CXX $inc $EXACT -c $d/$CS/tree.hip -o abv/$name/tree.o
+      $CXX $inc $EXACT -c $d/$CS/capi.hip -o abv/$name/capi.o
+      objs="abv/$name/tree.o abv/$name/capi.o"
+    else
+      $CXX -I $CS -I include $flags $RF -c ${src:-$CS/resnet.hip} -o abv/$name/resnet.o
+      objs="$B/tree.hip.o $B/capi.hip.o"
+    fi
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o abv/$name/liboamd.so abv/$name/resnet.o $objs
+    rm -rf abv/$name/*.o abv/$name/src
+    echo "built $name"
+  ) &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done
