@@ -138,7 +138,25 @@ def endgame_trajectory(m, case: dict, search) -> tuple[list, list]:
     return vis, qb
 
 
-def matching_runs(case: dict, vis: list, qb: list) -> int:
-    """How many of the reference's runs followed exactly this trajectory (0 =
-    none: the search is not one the reference produced)."""
-    return sum(t["count"] for t in case["trajectories"] if t["visits"] == vis and t["q_bits"] == qb)
+def matching_runs(case: dict, vis: list, qb: list) -> tuple[int, int]:
+    """(runs, ulp flips): how many of the reference's runs followed this
+    trajectory — every move's visit counts equal, Q within 1e-6 (SURVEY §4:
+    the reference's own Q moves by an ulp with its random_device symmetry
+    draws, which reorder the stub's float sums) — and how many Q values of the
+    best-matching run differ in their bits. (0, _) = no reference run
+    matches."""
+    def close(t):
+        if t["visits"] != vis:
+            return None
+        flips = 0
+        for a, b in zip(t["q_bits"], qb):
+            qa = np.array(a, np.uint32).view(np.float32)
+            qo = np.array(b, np.uint32).view(np.float32)
+            if np.abs(qa - qo).max(initial=0.0) > 1e-6:
+                return None
+            flips += int((qa != qo).sum())
+        return flips
+    hits = [(t["count"], f) for t in case["trajectories"] if (f := close(t)) is not None]
+    if not hits:
+        return 0, 0
+    return sum(c for c, _ in hits), min(f for _, f in hits)

@@ -4,8 +4,10 @@ Yardsticks: the reference's own AlphaZeroNet outputs (tests/golden/resnet.npz,
 fp32 torch CPU) and the fp32 torch restatement (oracle/resnet_ref.py) on the
 same inputs. The kernel computes in bf16 (or fp16) with fp32 accumulation and
 fp32 heads; tolerances (absolute, on probabilities / tanh values):
-  bf16: policy <= 2e-3, value <= 1e-2;  fp16: policy <= 5e-4, value <= 2e-3.
-Every case's measured maxima are printed in the terminal summary (numerics.py).
+  bf16: policy <= 5e-4, value <= 3e-3;  fp16: policy <= 1e-4, value <= 1e-3,
+about 3-5x the largest errors measured over every case here (round 2-3: bf16
+policy 9.8e-5 / value 9.6e-4, fp16 9.2e-6 / 2.3e-4). Every case's measured
+maxima are printed in the terminal summary (numerics.py).
 """
 
 import json
@@ -20,7 +22,7 @@ import resnet_ref
 pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda", 0)
-TOL = {"bf16": (2e-3, 1e-2), "fp16": (5e-4, 2e-3)}
+TOL = {"bf16": (5e-4, 3e-3), "fp16": (1e-4, 1e-3)}
 
 
 @pytest.fixture(scope="module")
@@ -189,24 +191,27 @@ def test_mcts_autodetects_alphazero_module(om):
 
 
 def test_pipeline_groups_do_not_change_results(om):
-    """Splitting the games over 1, 2, 3 or 8 stream groups is a pure scheduling
-    choice: every game's statistics must be identical."""
+    """Splitting the games over 1, 2, 3 or 8 stream groups, and letting the
+    groups' ResNet launches run as 1, 2 or 4 concurrent chains
+    (oamd_engine_set_nn_chains, bench --nn-chains), are pure scheduling
+    choices: every game's visits and Q must be identical."""
     from othello_mcts.synthetic import alphazero_state_dict
 
     net = om.NativeNet(alphazero_state_dict(17, 9, 128, 2, 32), device=0)
     kw = dict(history_size=4, num_simulations=96, num_threads=2, batch_size=8, seed=9,
               node_capacity=1 << 15)
     runs = []
-    for groups in (1, 2, 3, 8):
+    for groups, chains in ((1, 1), (2, 1), (3, 1), (8, 1), (2, 2), (4, 2), (8, 4)):
         b = om.BatchedMCTS(12, **kw)
         b.engine.set_pipeline(groups)
+        b.engine.set_nn_chains(chains)
         b.random_openings(5, seed=3)
         for _ in range(2):
             b.search(net)
             b.selfplay_move(temperature_moves=12, opening_moves=2)
         b.search(net)
         runs.append([(b.visit_counts(g), b.mean_action_values(g)) for g in range(12)])
-    assert runs[0] == runs[1] == runs[2] == runs[3]
+    assert all(r == runs[0] for r in runs[1:])
 
 
 def test_nn_batch_does_not_change_results(om):
