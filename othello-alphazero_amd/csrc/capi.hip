@@ -161,6 +161,7 @@ struct oamd_engine {
     float* spd_dev = nullptr;  // self-play data scratch (8*(1+2H)*64 + 8*65)
     // search state
     int steps_left = 0;
+    int steps_total = 0;  // of the step-wise search begun by oamd_engine_search_begin
     int step_phase = 0;  // 1 = a selected round awaits its backup (step API)
     // pipeline groups (0 = auto) and their streams / fork-join events
     int pipeline = 0;
@@ -792,6 +793,7 @@ int oamd_engine_reset(oamd_engine* e, int32_t game, uint64_t seed) {
 int oamd_engine_search_begin(oamd_engine* e, int32_t* steps) {
     const int L = e->L();
     e->steps_left = (e->cfg.num_simulations + L - 1) / L;  // search_thread.cpp:50-52
+    e->steps_total = e->steps_left;
     e->step_phase = 0;
     if (steps) *steps = e->steps_left;
     return OAMD_OK;
@@ -803,7 +805,8 @@ int oamd_engine_select(oamd_engine* e) {
     DeviceGuard dg(e->device);
     // a pending round is backed up thread by thread, each thread selecting its
     // next batch right after its backup (the reference's interleaving, k_tree)
-    launch_tree(e->view(), e->stream, e->step_phase == 1, true, e->cfg.num_threads, e->cfg.batch_size);
+    launch_tree(e->view(), e->stream, e->step_phase == 1, true, e->cfg.num_threads, e->cfg.batch_size, 0, -1, 0, -1,
+                nullptr, nullptr, e->steps_left == e->steps_total);
     LAUNCHCHK();
     e->step_phase = 1;
     e->steps_left -= 1;
@@ -935,7 +938,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * T + t)] : nullptr;
             if (s > 0) HIPCHK(hipStreamWaitEvent(e->stream, e->nn_ev[t], 0));  // thread t's batch s-1 evaluated
             if (ev) HIPCHK(hipEventRecord(ev[0], e->stream));
-            launch_tree(E, e->stream, s > 0, s < steps, T, B, 0, 1, t, t + 1);
+            launch_tree(E, e->stream, s > 0, s < steps, T, B, 0, 1, t, t + 1, nullptr, nullptr, s == 0);
             if (ev) HIPCHK(hipEventRecord(ev[1], e->stream));
             if (s == steps) continue;
             hipStream_t ns = e->pipe_stream[t % 2];
@@ -958,7 +961,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             // final round zeroes counter 0 for the next search's round 0
             int* cnt = e->rowcount + 2 * k;
             launch_tree(E, st[k], s > 0, s < steps, T, B, g0[k], ng[k], 0, -1, s < steps ? cnt + (s & 1) : nullptr,
-                        s < steps ? cnt + ((s + 1) & 1) : cnt);
+                        s < steps ? cnt + ((s + 1) & 1) : cnt, s == 0);
             if (ev) HIPCHK(hipEventRecord(ev[1], st[k]));
             if (s == steps) continue;
             // the groups' NN launches run one after another (OAMD_NN_ORDER)

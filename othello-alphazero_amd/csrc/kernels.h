@@ -23,10 +23,11 @@ struct SelfplayParams {
 // (do_backup), then select its next B leaves (do_select). T * B must equal
 // E.L. cnt_add: append the selected non-terminal rows to the evaluation list
 // E.rowlist[g0 * L ..] behind this counter; cnt_reset: the counter to zero
-// (the next round's). See tree.hip k_tree.
+// (the next round's). fresh: the search's first round (every virtual thread
+// starts with no batch selected). See tree.hip k_tree.
 void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
                  int g0 = 0, int ng = -1, int t0 = 0, int t1 = -1, int* cnt_add = nullptr,
-                 int* cnt_reset = nullptr);
+                 int* cnt_reset = nullptr, bool fresh = false);
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s);
 void launch_set_evaluation(const EngineView& E, const float* pol, const float* val, int row_begin,
                            int rows, hipStream_t s);

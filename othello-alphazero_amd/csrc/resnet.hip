@@ -62,6 +62,26 @@ constexpr int kMaxStampWgs = 1 << 16;
 // measured alternative: register staging, early stage opening, staggered or
 // prioritised waves, other DMA placements, 128-channel tiles, ...).
 constexpr int kStageBytes = 16384;
+// throughput geometries: stage bytes and ring slots per channel count.
+// Edge-row boards without their never-read top / bottom border rows leave
+// room for a fourth 16 KiB slot or for 32 KiB stages. Same box, 4096 rows
+// (profiles/r03/ab): C=256 with 4 slots (3 stages in flight) 6.60 ms vs 6.75
+// with 3; 32 KiB stages in 2 slots (one barrier per 2 K-steps) 7.13-7.22 vs
+// 6.69. C=128: 4 slots 0.81-0.83 vs 0.78, 32 KiB stages 0.83-0.84 vs 0.78.
+#ifndef OAMD_C128_STAGE
+#define OAMD_C128_STAGE 16384
+#endif
+#ifndef OAMD_C128_RING
+#define OAMD_C128_RING 3
+#endif
+#ifndef OAMD_C256_STAGE
+#define OAMD_C256_STAGE 16384
+#endif
+#ifndef OAMD_C256_RING
+#define OAMD_C256_RING 4
+#endif
+constexpr int kStageBytesMax = 32768;
+__host__ __device__ constexpr int stage_bytes(int C) { return C == 256 ? OAMD_C256_STAGE : OAMD_C128_STAGE; }
 // k_resnet_w8 register cap: gfx950 counts the unified VGPR+AGPR file, the
 // backend doubles this value: 2 x 104 = 208 VGPRs, so one 96-VGPR k_tree wave
 // fits beside the two ResNet waves of a SIMD
@@ -107,7 +127,7 @@ size_t resnet_head_floats(int C, int hidden) { return (size_t)HeadLayout(C, hidd
 
 // ---- K-step schedule (shared with the host packer) --------------------------
 __host__ __device__ constexpr int ksteps_per_stage(int C) {
-    return kStageBytes / (32 * C * 2);
+    return stage_bytes(C) / (32 * C * 2);
 }
 __host__ __device__ constexpr int ksteps_first(int C) {
     return (9 + ksteps_per_stage(C) - 1) / ksteps_per_stage(C) * ksteps_per_stage(C);
@@ -145,7 +165,7 @@ size_t resnet_packed_weight_elems(int C, int R) {
 }
 // + a zero pad of 4 stages: the weight stream runs up to AHEAD (<= 3) stages
 // past the last one (issue_stage_dma)
-size_t resnet_packed_weight_alloc_elems(int C, int R) { return resnet_packed_weight_elems(C, R) + 4 * kStageBytes / 2; }
+size_t resnet_packed_weight_alloc_elems(int C, int R) { return resnet_packed_weight_elems(C, R) + 4 * kStageBytesMax / 2; }
 
 // ---- activation layout --------------------------------------------------------
 // padded row of board position p = 8y + x inside its board's 10x10 grid
@@ -173,31 +193,34 @@ constexpr TilePos make_tile_pos() {
 }
 __constant__ TilePos kTilePos = make_tile_pos();
 
-// Edge-row tiling (G::EDGE): padded row of B-fragment column j of position tile
+// Edge-row tiling (G::EDGE): layout row of B-fragment column j of position tile
 // m for position group q (wave / WN). Group q = (pair P, half h): tile m is
-// board row y = h ? 7 - m : m of boards P and P + NPAIR (NPAIR * BROWS = 8 mod
-// 16 rows apart, so the tile's 16 squares cover every residue of the padded row
-// mod 16 once). Columns 0-3 / 12-15 take the odd-residue squares of board P /
+// board row y = 4h + m of boards P and P + NPAIR (NPAIR * BROWS = 8 mod 16 rows
+// apart, so the tile's 16 squares cover every residue of the layout row mod 16
+// once). Columns 0-3 / 12-15 take the odd-residue squares of board P /
 // P + NPAIR, columns 4-7 / 8-11 the even ones: the kTilePos split, so the
 // kgroup_chunk map keeps every ds_read_b128 lane group on 16 distinct slots
-// (tests/test_cpu_host.py restates and checks it for every tap).
+// (tests/test_cpu_host.py restates and checks it for every tap). Edge-row
+// boards keep no top / bottom border rows (G::ROW0 = 0): the MFMAs of tile 0
+// at dy = -1 and tile 7 at dy = +1 are left out, so rows -1 and 8 are never
+// read; the left / right border columns stay (zero) in every row.
 template <class G>
 __host__ __device__ constexpr int edge_tile_row(int q, int m, int j) {
     constexpr int NP = G::NPAIR > 0 ? G::NPAIR : 1;
     const int P = q % NP, h = q / NP;
     const int y = 4 * h + m;
-    const int r0 = (P * G::BROWS + (y + 1) * 10 + 1) & 15;
+    const int r0 = (P * G::BROWS + G::ROW0 + y * 10 + 1) & 15;
     const int oddcol = (j < 4 || j >= 12) ? 1 : 0;
     const int b = j < 8 ? P : P + NP;
     const int x = 2 * (j & 3) + ((r0 & 1) ^ oddcol);
-    return b * G::BROWS + (y + 1) * 10 + x + 1;
+    return b * G::BROWS + G::ROW0 + y * 10 + x + 1;
 }
 
 // Workgroup geometry: C channels, BOARDS boards per workgroup, WC output
 // channels per wave (NT = WC/16 MFMA tiles), at most RING_MAX weight slots of
 // STAGE bytes (a whole number of K-steps; the packed weights are K-step
 // granular, so any stage size reads the same buffer).
-template <int C_, int BOARDS_, int WC_, int RING_MAX_, int STAGE_ = kStageBytes, int PW_ = 64>
+template <int C_, int BOARDS_, int WC_, int RING_MAX_, int STAGE_ = stage_bytes(C_), int PW_ = 64>
 struct GeoT {
     static constexpr int C = C_;
     static constexpr int BOARDS = BOARDS_;
@@ -212,11 +235,16 @@ struct GeoT {
     static constexpr int RP = 2 * C + 16;       // row pitch (bytes)
     // board stride in rows (10x10 padded board); with two boards per workgroup
     // 104, so the two boards of an edge tile sit 8 rows apart modulo 16
-    static constexpr int BROWS = BOARDS_ == 2 ? 104 : 100;
     static constexpr int NPAIR = BOARDS / 2;
     // edge-row wave tiles (32 channels x rows 0-7 of a board pair)
-    static constexpr bool EDGE = BOARDS >= 2 && BOARDS % 2 == 0 && WC_ == 32 && PW_ == 128 &&
-                                 (STAGE_ == 2 * 32 * C_ * 2 || STAGE_ == 32 * C_ * 2);
+    static constexpr bool EDGE = BOARDS >= 2 && BOARDS % 2 == 0 && WC_ == 32 && PW_ == 128;
+    // layout row of board row y, column x (x = -1, 8: the zero border) is
+    // b * BROWS + ROW0 + 10 y + x + 1. Edge-row boards: 8 rows of 10 (no top /
+    // bottom border), BROWS = 84 / 88 so the boards of a tile pair sit 8 rows
+    // apart mod 16; other geometries: the full 10 x 10 bordered board
+    static constexpr int ROW0 = EDGE ? 0 : 10;
+    static constexpr int BROWS = !EDGE ? 100 : (NPAIR == 1 ? 88 : 84);
+    __host__ __device__ static constexpr int prow(int p) { return ROW0 + (p >> 3) * 10 + (p & 7) + 1; }
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
     static constexpr int KSTEP_BYTES = 32 * C * 2;
     static constexpr int STAGE = STAGE_;
@@ -244,7 +272,8 @@ struct GeoT {
     // the stage's second K-step issues (1, SPLIT_DMA only)
     static constexpr int OPEN_PART = SPLIT_DMA ? 0 : -1;
     static constexpr int MID_PART = 1;
-    static_assert(RING >= 3 && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
+    static_assert(RING >= 2 && LDS <= kLdsBytes && STAGE == KS * KSTEP_BYTES, "LDS budget");
+    static_assert(KS == 1 || KS == 2 || KS == 4, "K-steps per stage");
     static_assert(ksteps_first(C) % KS == 0 && ksteps_tower(C) % KS == 0, "whole stages per layer");
     static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 63, "decomposition");
     static_assert(!EDGE || ((NPAIR * BROWS) % 16 == 8 && WAVES == 8), "edge tiles: pair boards 8 rows apart mod 16");
@@ -252,7 +281,7 @@ struct GeoT {
 // throughput geometry: 512 positions x C channels per workgroup, 8 waves of
 // 32 channels x 128 positions (edge-row tiles)
 template <int C>
-using Geo = GeoT<C, 512 / C, 32, 3, kStageBytes, 128>;
+using Geo = GeoT<C, 512 / C, 32, C == 128 ? OAMD_C128_RING : OAMD_C256_RING, stage_bytes(C), 128>;
 // small-batch geometry (latency): one board per workgroup, 8 waves of C/8
 // channels, so a handful of rows spreads over as many CUs as boards. 8 waves
 // take 0.098 ms per 16-32 rows against 0.107 with 4 (two same-box pairs,
@@ -260,7 +289,7 @@ using Geo = GeoT<C, 512 / C, 32, 3, kStageBytes, 128>;
 // fragment reads per MFMA, sets the time; a 4-, 6- or 8-slot ring measured
 // equal
 template <int C>
-using GeoS = GeoT<C, 1, C / 8, 4>;
+using GeoS = GeoT<C, 1, C / 8, 4, kStageBytes>;
 
 template <int DT>
 __device__ __forceinline__ uint32_t to_act(float v) {
@@ -535,7 +564,7 @@ __device__ __forceinline__ void heads(const NetView& N, const unsigned char* act
         int rd[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
-            rd[m] = (b * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) * G::RP + kgroup_chunk(lane >> 4) * 16;
+            rd[m] = (b * G::BROWS + G::prow(kTilePos.p[16 * m + (lane & 15)])) * G::RP + kgroup_chunk(lane >> 4) * 16;
         f32x4_t d[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) d[m] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
@@ -683,7 +712,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 #pragma unroll
     for (int m = 0; m < kMT; ++m) {
         const int rowb = (G::EDGE ? edge_tile_row<G>(wm, m, lane & 15)
-                                  : wm * G::BROWS + pad_row(kTilePos.p[16 * m + (lane & 15)])) *
+                                  : wm * G::BROWS + G::prow(kTilePos.p[16 * m + (lane & 15)])) *
                          G::RP;
         rd[m] = rowb + kgroup_chunk(kg) * 16;
         wr[m] = rowb;
@@ -691,9 +720,13 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     const int wl = (wn * kNT * 64 + lane) * 16;
 
     // ---------------- zero border rows; input planes -> channels 0..31 ------
-    for (int w = tid; w < G::BOARDS * 36 * (C / 8); w += G::THREADS) {
-        const int c = w % (C / 8), k = (w / (C / 8)) % 36, b = w / (C / 8) / 36;
-        const int r = k < 10 ? k : (k < 20 ? 80 + k : ((k - 20) >> 1) * 10 + 10 + ((k & 1) ? 9 : 0));
+    // border cells per board: bordered boards 10 top + 10 bottom + 16 side,
+    // edge-row boards only the 16 side cells (x = -1, 8 of rows 0-7)
+    constexpr int NBC = G::ROW0 ? 36 : 16;
+    for (int w = tid; w < G::BOARDS * NBC * (C / 8); w += G::THREADS) {
+        const int c = w % (C / 8), k = (w / (C / 8)) % NBC, b = w / (C / 8) / NBC;
+        const int r = G::ROW0 ? (k < 10 ? k : (k < 20 ? 80 + k : ((k - 20) >> 1) * 10 + 10 + ((k & 1) ? 9 : 0)))
+                              : (k >> 1) * 10 + ((k & 1) ? 9 : 0);
         *reinterpret_cast<u32x4_t*>(act + (b * G::BROWS + r) * G::RP + c * 16) = u32x4_t{0u, 0u, 0u, 0u};
     }
     if (tid < G::BOARDS * 64) {
@@ -748,7 +781,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 words[w] = lo | (hi << 16);
             }
         }
-        unsigned char* dst = act + (b * G::BROWS + pad_row(p)) * G::RP;
+        unsigned char* dst = act + (b * G::BROWS + G::prow(p)) * G::RP;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
             *reinterpret_cast<u32x4_t*>(dst + c * 16) =
@@ -790,7 +823,11 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     // stage 0 and the input planes must be visible (bias loads are older than the DMAs)
     wait_vm<G::VM_LAYER>();
     lds_barrier();
-    load_frags(fa, act, ring, first_kstep_offset<C>(0), rd, wl);
+    // the first conv's K-step 0 (tap 0, dy = -1: edge-row geometries skip tile 0)
+    load_wfrags(fa, ring, wl);
+#pragma unroll
+    for (int m = kWide ? 1 : 0; m < kMT; ++m)
+        fa.x[m] = *reinterpret_cast<const u32x4_t*>(act + first_kstep_offset<C>(0) + rd[m]);
     OAMD_STAMP(1);
     // throughput geometry: every ResNet wave issues ahead of the other pipeline
     // group's co-resident tree waves (SQ arbitration): bench C2 4.42-4.47 vs
@@ -825,10 +862,17 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             }
 
         // step: load K-step i1's fragments into nxt, then MFMAs on cur (K-step
-        // i1-1). NEW: i1 opens a new stage -> DMA wait + barrier, ring advances.
-        // xoff: uniform byte offset of the next K-step's activation rows/channels
-        auto step = [&](auto NEW, const Frags<kNT, kMT>& cur, Frags<kNT, kMT>& nxt, int xoff) {
-            constexpr bool open = decltype(NEW)::value;
+        // i1-1). KIS: i1's K-step within its stage (0: i1 opens a new stage ->
+        // DMA wait + barrier, ring advances). TILES = xlo | xhi << 4 | mlo << 8 |
+        // mhi << 12: position tiles [xlo, xhi) of nxt are read and MFMAs run on
+        // tiles [mlo, mhi) of cur (edge-row geometries leave out the border
+        // tiles of the first conv). xoff: uniform byte offset of the next
+        // K-step's activation rows/channels
+        auto step = [&](auto KIS, auto TILES, const Frags<kNT, kMT>& cur, Frags<kNT, kMT>& nxt, int xoff) {
+            constexpr int kis = decltype(KIS)::value;
+            constexpr bool open = kis == 0;
+            constexpr int tl = decltype(TILES)::value;
+            constexpr int xlo = tl & 15, xhi = (tl >> 4) & 15, mlo = (tl >> 8) & 15, mhi = (tl >> 12) & 15;
             // keep each step's MFMAs (on cur) with the fragment reads they hide:
             // without this fence the scheduler may hoist the next step's MFMAs over
             // the barrier right behind their reads and drain lgkmcnt each step
@@ -840,7 +884,11 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             // activation fragments do not depend on the stage barrier (the
             // layer's input is fixed): issued before it, their latency overlaps
             // the barrier wait (+3.6 %)
-            load_xfrags(nxt, act, xoff, rd);
+            {
+                const unsigned char* ap = act + xoff;
+#pragma unroll
+                for (int m = xlo; m < xhi; ++m) nxt.x[m] = *reinterpret_cast<const u32x4_t*>(ap + rd[m]);
+            }
             if constexpr (open) {
                 // open the next stage: it has landed (this wave's DMAs, then
                 // everyone's via the barrier), and the slot of the stage before the
@@ -858,15 +906,17 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 sa = sa >= G::RING ? sa - G::RING : sa;
                 issue_stage_dma<G, G::MID_PART>(wcur, ring, sa, tid);
             }
-            constexpr int kis = open ? 0 : 1;  // K-step within its stage
             load_wfrags(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
-            mfma_frags<DT>(acc, cur);
+#pragma unroll
+            for (int n = 0; n < kNT; ++n)
+#pragma unroll
+                for (int m = mlo; m < mhi; ++m) acc[n][m] = mfma<DT>(cur.w[n], cur.x[m], acc[n][m]);
             // fine interleave of the step's fragment reads with its MFMAs (one
             // read, then a share of the MFMAs; +2.5 %): a stage-opening step has
             // only its weight reads after the barrier
             if constexpr (kMT != 4) {
-                constexpr int nds = open ? kNT : kNT + kMT;
-                constexpr int nm = kNT * kMT;
+                constexpr int nds = open ? kNT : kNT + (xhi - xlo);
+                constexpr int nm = kNT * (mhi - mlo);
                 static_for<nds>([&](auto I) {
                     constexpr int i = decltype(I)::value;
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -880,23 +930,34 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 });
             }
         };
-        using NewOdd = std::integral_constant<bool, G::KS == 1>;  // K-step i1 odd
-        using NewEven = std::integral_constant<bool, true>;       // K-step i1 even
+        // all tiles read and multiplied
+        using AllTiles = std::integral_constant<int, kMT << 4 | kMT << 12>;
         if constexpr (first) {
-            int i = 0;
-            for (; i + 2 < nk; i += 2) {
-                step(NewOdd{}, fa, fb, first_kstep_offset<C>(i + 1));
-                step(NewEven{}, fb, fa, first_kstep_offset<C>(i + 2));
-            }
-            if constexpr (nk % 2 == 0) {
-                step(NewOdd{}, fa, fb, first_kstep_offset<C>(nk - 1));
-                mfma_frags<DT>(acc, fb);
-            } else {
-                mfma_frags<DT>(acc, fa);
-            }
+            // tap-major, K-step i = tap min(i, 8) (the pad steps repeat tap 8
+            // with zero weights); edge-row geometries leave out tile 0 at
+            // dy = -1 and tile 7 at dy = +1 (rows -1 and 8 are not in the layout)
+            auto tiles = [](int i) {
+                const int dy = (i < 9 ? i : 8) / 3 - 1;
+                const int lo = kWide && dy < 0 ? 1 : 0, hi = kWide && dy > 0 ? kMT - 1 : kMT;
+                return lo | hi << 4 | lo << 8 | hi << 12;
+            };
+            static_for<nk - 1>([&](auto II) {
+                constexpr int i1 = decltype(II)::value + 1;  // the K-step this step loads
+                constexpr int tl = (tiles(i1) & 0xFF) | (tiles(i1 - 1) & 0xFF00);
+                if constexpr (i1 % 2 == 1) step(std::integral_constant<int, i1 % G::KS>{},
+                                                std::integral_constant<int, tl>{}, fa, fb, first_kstep_offset<C>(i1));
+                else step(std::integral_constant<int, i1 % G::KS>{}, std::integral_constant<int, tl>{}, fb, fa,
+                          first_kstep_offset<C>(i1));
+            });
+            constexpr int ml = tiles(nk - 1) >> 8 & 15, mh = tiles(nk - 1) >> 12 & 15;
+            const Frags<kNT, kMT>& last = (nk - 1) % 2 == 1 ? fb : fa;
+#pragma unroll
+            for (int n = 0; n < kNT; ++n)
+#pragma unroll
+                for (int m = ml; m < mh; ++m) acc[n][m] = mfma<DT>(last.w[n], last.x[m], acc[n][m]);
         } else if constexpr (kWide) {
             constexpr int KPT = C / 32;
-            static_assert(kNT == 2 && kMT == 8 && KPT % 2 == 0 && (G::KS == 1 || G::KS == 2), "wide geometry");
+            static_assert(kNT == 2 && kMT == 8 && KPT % 2 == 0 && (3 * KPT) % G::KS == 0, "wide geometry");
             constexpr int NJ = 3 * KPT;     // K-steps per dx
             constexpr int RS = 10 * G::RP;  // one board row
             // K-step J = (cb J/3, dy J%3 - 1) of the dx: tiles mlo..mhi-1 from
@@ -907,7 +968,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             auto wstep = [&](auto JJ, const Frags<kNT, kMT>& wc, Frags<kNT, kMT>& wn, int sbn) {
                 constexpr int J = decltype(JJ)::value;
                 constexpr int Jn = (J + 1) % NJ;
-                constexpr bool open = G::KS == 1 || Jn % 2 == 0;
+                constexpr bool open = Jn % G::KS == 0;
                 constexpr int dy = wide_dy(J), cbn = wide_cb(Jn), nnew = __builtin_popcount(wide_new(Jn));
                 constexpr int mlo = dy < 0 ? 1 : 0, mhi = dy > 0 ? 7 : 8;
                 auto& Wc = [&]() -> u32x4_t(&)[9] {
@@ -935,7 +996,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     sa = sa >= G::RING ? sa - G::RING : sa;
                     issue_stage_dma<G, G::MID_PART>(wcur, ring, sa, tid);
                 }
-                load_wfrags(wn, ring + slot * G::STAGE + (open ? 0 : G::KSTEP_BYTES), wl);
+                load_wfrags(wn, ring + slot * G::STAGE + (Jn % G::KS) * G::KSTEP_BYTES, wl);
 #pragma unroll
                 for (int n = 0; n < kNT; ++n)
 #pragma unroll
@@ -979,10 +1040,10 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 constexpr bool lastdx = decltype(LASTDX)::value;
                 static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
                     constexpr int J = decltype(JJ)::value;
-                    using NEW = std::integral_constant<bool, G::KS == 1 || (J + 1) % 2 == 0>;
+                    using KIS = std::integral_constant<int, (J + 1) % G::KS>;
                     const int xo = J == NJ - 1 ? xoff_of(dxi + 1, 0) : xoff_of(dxi, J + 1);
-                    if constexpr (J % 2 == 0) step(NEW{}, fa, fb, xo);
-                    else step(NEW{}, fb, fa, xo);
+                    if constexpr (J % 2 == 0) step(KIS{}, AllTiles{}, fa, fb, xo);
+                    else step(KIS{}, AllTiles{}, fb, fa, xo);
                 });
             };
 #pragma nounroll

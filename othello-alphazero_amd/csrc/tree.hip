@@ -478,7 +478,7 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
 // behind the counter *cnt_add; *cnt_reset (the counter of the next round,
 // which no launch still reads) is zeroed by the group's first wave.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree(EngineView E, int g0, int do_backup, int do_select,
-                                             int t0, int t1, int B, int* cnt_add, int* cnt_reset) {
+                                             int t0, int t1, int B, int* cnt_add, int* cnt_reset, int fresh) {
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
         // virtual thread t: batches selected so far in this search, and whether
         // its last batch waits for the NN (a search's first round starts fresh)
         int* ts = E.tstate + (size_t)g * E.L + t;
-        const int st = do_backup ? *ts : 0;
+        const int st = fresh ? 0 : *ts;
         int sel = st & 0xFFFF;
         bool pend = (st >> 16) & 1;
         if (do_backup && pend) {
@@ -942,13 +942,13 @@ __global__ void k_apply_positions(const Pos* in, const int32_t* actions, Pos* ou
 static inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
-                 int g0, int ng, int t0, int t1, int* cnt_add, int* cnt_reset) {
+                 int g0, int ng, int t0, int t1, int* cnt_add, int* cnt_reset, bool fresh) {
     if (ng < 0) ng = E.G - g0;
     if (t1 < 0) t1 = T;
     if (T * B != E.L || t0 < 0 || t1 > T || t0 >= t1) return;  // caller validated; never launch on a mismatched layout
     if (ng > 0 && (do_backup || do_select))
         hipLaunchKernelGGL(k_tree, dim3(ng), dim3(64), 0, s, E, g0, (int)do_backup, (int)do_select, t0, t1, B,
-                           do_select ? cnt_add : nullptr, cnt_reset);
+                           do_select ? cnt_add : nullptr, cnt_reset, (int)fresh);
 }
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s) {
     if (rows > 0) hipLaunchKernelGGL(k_features_f32, dim3(blocks_for(rows, 4)), dim3(256), 0, s, E, out, row_begin, rows);

@@ -204,25 +204,46 @@ def test_resnet_activation_layout_is_bank_conflict_free():
     # edge-row tiling (edge_tile_row): tile m of position group q is board row
     # y = 4h + m of boards P and P + NPAIR; the kernel's 128-position waves (PW
     # 128) own rows 0-7 of their pair (64-position waves, rows 0-3 / 4-7 of a
-    # half, are checked too: the layout serves both)
+    # half, are checked too: the layout serves both). Edge-row boards keep no
+    # top / bottom border rows (GeoT::ROW0 = 0, BROWS 84 / 88 so that the
+    # boards of a pair sit 8 rows apart mod 16): only reads of board rows 0-7
+    # happen (tile 0 at dy = -1 and tile 7 at dy = +1 are left out)
+    def edge_stride(C):
+        return 88 if 512 // C == 2 else 84
+
     def edge_tile_row(C, q, m, j):
         npair = 512 // C // 2
         P, h = q % npair, q // npair
         y = 4 * h + m
-        r0 = (P * stride(C) + (y + 1) * 10 + 1) & 15
+        r0 = (P * edge_stride(C) + y * 10 + 1) & 15
         oddcol = 1 if (j < 4 or j >= 12) else 0
         b = P if j < 8 else P + npair
         x = 2 * (j & 3) + ((r0 & 1) ^ oddcol)
-        return b, y, x, b * stride(C) + (y + 1) * 10 + x + 1
+        return b, y, x, b * edge_stride(C) + y * 10 + x + 1
+
+    def edge_conflict_free(C, rows, y):
+        pitch = 2 * C + 16
+        for t in range(9):
+            dy, dx = t // 3 - 1, t % 3 - 1
+            if not 0 <= y + dy <= 7:
+                continue  # a border tile: its MFMAs and reads are left out
+            for kc in range(C // 32):
+                for g in groups:
+                    addrs = [(rows[lane & 15] + dy * 10 + dx) * pitch + (kc * 4 + chunk(lane >> 4)) * 16 for lane in g]
+                    if len({(a // 16) % 16 for a in addrs}) != 16:
+                        return False
+        return True
 
     for C in (128, 256):
         boards = 512 // C
+        assert (boards // 2 * edge_stride(C)) % 16 == 8 and edge_stride(C) >= 80
+        assert boards * edge_stride(C) * (2 * C + 16) + (4 if C == 256 else 3) * 16384 <= 160 * 1024
         for pw in (64, 128):
             seen = set()
             for q in range(boards * 64 // pw):
                 for m in range(pw // 16):
                     sq = [edge_tile_row(C, q, m, j) for j in range(16)]
-                    assert conflict_free(C, [r for *_, r in sq])
+                    assert edge_conflict_free(C, [r for *_, r in sq], sq[0][1])
                     assert len({y for _, y, _, _ in sq}) == 1
                     seen |= {(b, y, x) for b, y, x, _ in sq}
                     assert sq[0][1] == 4 * (q // (boards // 2)) + m  # ascending rows
@@ -230,6 +251,12 @@ def test_resnet_activation_layout_is_bank_conflict_free():
                     # reads row r of the wave as base + r board rows
                     r0 = [edge_tile_row(C, q, 0, j)[3] for j in range(16)]
                     assert [r - 10 * m for *_, r in sq] == r0
+                    # every tap a kept tile reads stays inside its own board's rows
+                    for t in range(9):
+                        dy, dx = t // 3 - 1, t % 3 - 1
+                        if 0 <= sq[0][1] + dy <= 7:
+                            for b, y, x, r in sq:
+                                assert b * edge_stride(C) <= r + dy * 10 + dx < b * edge_stride(C) + 80
             assert seen == {(b, y, x) for b in range(boards) for y in range(8) for x in range(8)}
 
 
