@@ -266,6 +266,9 @@ def parse_args(argv: list[str]):
                          "configs[4] uses 2048")
     ap.add_argument("--pipeline", type=int, default=0, help="pipeline groups (0 = engine default: 2)")
     ap.add_argument("--nn-chains", type=int, default=1, help="concurrent chains of ResNet launches")
+    ap.add_argument("--round-robin-endgames", action="store_true",
+                    help="all-terminal batches wait for their round instead of the reference's immediate "
+                         "re-selection (oamd_engine_set_exact_interleaving(0)); default: exact")
     ap.add_argument("--cpu-baseline-moves", type=int, default=24,
                     help="timed moves of the CPU baseline (0 = skip it), after 2 warm-up moves")
     ap.add_argument("--cpu-baseline-threads", type=int, default=0,
@@ -352,6 +355,7 @@ class EngineWorkload:
         if args.pipeline:
             self.b.engine.set_pipeline(args.pipeline)
         self.b.engine.set_nn_chains(args.nn_chains)
+        self.b.engine.set_exact_interleaving(not args.round_robin_endgames)
         props = torch.cuda.get_device_properties(local)
         self.device_id = f"{os.uname().nodename}:{getattr(props, 'uuid', local)}"
 
@@ -433,6 +437,7 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
                                if n_devices < world else "")),
             "ranks": ranks,
             "backend": (backend if world > 1 else "none"),
+            "endgame_interleaving": "round-robin" if args.round_robin_endgames else "exact (reference)",
         },
     }
     if args.dry_run:

@@ -176,6 +176,15 @@ int oamd_engine_set_nn_batch(oamd_engine *e, int32_t rows);
  * k % chains, 1..4, default 1): launches of one chain run one after another,
  * chains run concurrently. Results do not depend on it. */
 int oamd_engine_set_nn_chains(oamd_engine *e, int32_t chains);
+/* enable = 1 (default): the reference's thread interleaving exactly — a
+ * virtual thread whose batch is all terminal backs it up without an NN round
+ * trip and selects again at once (search_thread.cpp:102-127), in the same
+ * round. enable = 0: such a batch waits for its thread's next round like any
+ * other (the round-robin of round 2): identical results until a batch is all
+ * terminal (endgames), and no round longer than one batch per thread, so the
+ * search rounds stay hidden behind the other pipeline group's ResNet launch
+ * in sustained self-play. */
+int oamd_engine_set_exact_interleaving(oamd_engine *e, int32_t enable);
 /* Diagnostics: copy the ResNet kernel's per-workgroup time stamps (8 u64 per
  * workgroup, 16 u64 per workgroup: see tools/nn_stamps.py) of the last launch. Only in builds
  * with OAMD_EXTRA_FLAGS=-DOAMD_STAMPS; otherwise OAMD_INVALID_ARGUMENT. */

@@ -162,6 +162,7 @@ struct oamd_engine {
     // search state
     int steps_left = 0;
     int steps_total = 0;  // of the step-wise search begun by oamd_engine_search_begin
+    bool exact_interleaving = true;  // oamd_engine_set_exact_interleaving
     int step_phase = 0;  // 1 = a selected round awaits its backup (step API)
     // pipeline groups (0 = auto) and their streams / fork-join events
     int pipeline = 0;
@@ -293,6 +294,7 @@ struct oamd_engine {
         E.tstate = tstate;
         E.steps = (cfg.num_simulations + L() - 1) / L();
         E.B = cfg.batch_size;
+        E.terminal_skip = exact_interleaving ? 1 : 0;
         return E;
     }
 
@@ -1056,6 +1058,11 @@ int oamd_engine_set_nn_chains(oamd_engine* e, int32_t chains) {
     if (chains < 1 || chains > oamd_engine::kMaxChains)
         return fail(OAMD_INVALID_ARGUMENT, "nn chains must be in [1, " + std::to_string(oamd_engine::kMaxChains) + "]");
     e->nn_chains = chains;
+    return OAMD_OK;
+}
+
+int oamd_engine_set_exact_interleaving(oamd_engine* e, int32_t enable) {
+    e->exact_interleaving = enable != 0;
     return OAMD_OK;
 }
 

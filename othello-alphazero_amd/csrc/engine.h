@@ -74,6 +74,8 @@ struct EngineView {
     int32_t* tstate;   // G*L (entry g*L + t for virtual thread t): batches selected | pending << 16
     int32_t steps;     // batches per virtual thread and search: ceil(num_simulations / L)
     int32_t B;         // batch_size (leaves per virtual thread and batch)
+    int32_t terminal_skip;  // 1: an all-terminal batch is backed up at once and its thread selects
+                            // again (the reference's interleaving); 0: it waits for its round
 };
 
 }  // namespace oamd

@@ -524,7 +524,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
             select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals, cnt_add,
                          g0 * E.L);
             ++sel;
-            if (evals != ev0) pend = true;
+            if (evals != ev0 || !E.terminal_skip) pend = true;
             else backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
         }
         if (lane == 0) *ts = sel | (pend ? 1 << 16 : 0);

@@ -186,7 +186,8 @@ def _pos(b, g):
     return O.CPos(i["player"], i["player1_discs"], i["player2_discs"], i["legal_moves"], i["next_legal_moves"])
 
 
-def test_evaluation_lists_through_endgames(om):
+@pytest.mark.parametrize("exact", [True, False], ids=["exact", "round_robin"])
+def test_evaluation_lists_through_endgames(om, exact):
     """The native search evaluates only the rows of non-terminal leaves (the
     per-group evaluation lists of tree.hip append_rows, read by the ResNet
     launch): through whole games, restarts and endgames full of terminal
@@ -200,6 +201,9 @@ def test_evaluation_lists_through_endgames(om):
               node_capacity=1 << 16)
     a, c, e = om.BatchedMCTS(64, **kw), om.BatchedMCTS(64, **kw), om.BatchedMCTS(64, **kw)
     e.engine.set_nn_batch(384)
+    if not exact:  # all-terminal batches wait for their round (oamd_engine_set_exact_interleaving)
+        for x in (a, c, e):
+            x.engine.set_exact_interleaving(False)
     for x in (a, c, e):
         x.random_openings(8, seed=6)
     total_sims = total_evals = 0
@@ -220,6 +224,7 @@ def test_evaluation_lists_through_endgames(om):
         xe = e.selfplay_move(temperature_moves=12, opening_moves=4)["actions"]
         assert torch.equal(xa, xc) and torch.equal(xa, xe), mv
     share = 1.0 - total_evals / total_sims
-    numerics.record("evaluation lists", f"64 games x 75 moves: terminal-leaf share {share:.3f}, "
-                                        "native (lists, eval batch 0 / 384) == callback")
+    numerics.record(f"evaluation lists ({'exact' if exact else 'round-robin'} endgames)",
+                    f"64 games x 75 moves: terminal-leaf share {share:.3f}, "
+                    "native (lists, eval batch 0 / 384) == callback")
     assert share > 0.02  # the endgames were reached
