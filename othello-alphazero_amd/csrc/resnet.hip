@@ -80,6 +80,15 @@ constexpr int kStageBytes = 16384;
 #ifndef OAMD_C256_RING
 #define OAMD_C256_RING 4
 #endif
+// C=256 throughput geometry: weight fragments go from global memory (L2)
+// straight into a per-wave register queue 3 K-steps ahead of their MFMAs
+// instead of through the LDS ring (GeoT::DIRECT): no stage barriers (the ring
+// needs one per K-step at C=256). Same box, 4096 rows (profiles/r03/ab):
+// 6.385 ms vs 6.725 with the ring; a 2-deep queue 6.51; 6- and 8-deep queues
+// spill. At C=128 (one barrier per 2 K-steps, and the two board pairs' waves
+// of a channel block fetch the same fragments) the queue measured 1.3 %
+// slower than the ring: 0.807-0.809 vs 0.794-0.798 ms.
+constexpr int kWeightQueue = 4;
 constexpr int kStageBytesMax = 32768;
 __host__ __device__ constexpr int stage_bytes(int C) { return C == 256 ? OAMD_C256_STAGE : OAMD_C128_STAGE; }
 // k_resnet_w8 register cap: gfx950 counts the unified VGPR+AGPR file, the
@@ -246,6 +255,10 @@ struct GeoT {
     static constexpr int BROWS = !EDGE ? 100 : (NPAIR == 1 ? 88 : 84);
     __host__ __device__ static constexpr int prow(int p) { return ROW0 + (p >> 3) * 10 + (p & 7) + 1; }
     static constexpr int ACT_BYTES = BOARDS * BROWS * RP;
+    // DIRECT: no weight ring during the tower (its LDS stays allocated as the
+    // heads' scratch); WQ = K-steps of weight fragments held per wave
+    static constexpr bool DIRECT = EDGE && C == 256;
+    static constexpr int WQ = kWeightQueue;
     static constexpr int KSTEP_BYTES = 32 * C * 2;
     static constexpr int STAGE = STAGE_;
     static constexpr int KS = STAGE / KSTEP_BYTES;
@@ -277,6 +290,7 @@ struct GeoT {
     static_assert(ksteps_first(C) % KS == 0 && ksteps_tower(C) % KS == 0, "whole stages per layer");
     static_assert(THREADS >= BOARDS * 64 && DPT >= 1 && VM_LAYER <= 63, "decomposition");
     static_assert(!EDGE || ((NPAIR * BROWS) % 16 == 8 && WAVES == 8), "edge tiles: pair boards 8 rows apart mod 16");
+    static_assert(!DIRECT || ((3 * (C / 32)) % WQ == 0 && WQ >= 2), "register queue: whole queues per dx");
 };
 // throughput geometry: 512 positions x C channels per workgroup, 8 waves of
 // 32 channels x 128 positions (edge-row tiles)
@@ -698,26 +712,48 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 
     // weight stream starts right away: stages 0 .. AHEAD (with SPLIT_DMA the
     // newest stage's second piece goes out at stage 0's second K-step)
-#pragma unroll
-    for (int s = 0; s < G::AHEAD; ++s) issue_stage_dma<G>(wsrc + s * G::STAGE, ring, s, tid);
     const unsigned char* wcur = wsrc + G::AHEAD * G::STAGE;  // the newest stage issued
-    issue_stage_dma<G, G::OPEN_PART>(wcur, ring, G::AHEAD, tid);
+    if constexpr (!G::DIRECT) {
+#pragma unroll
+        for (int s = 0; s < G::AHEAD; ++s) issue_stage_dma<G>(wsrc + s * G::STAGE, ring, s, tid);
+        issue_stage_dma<G, G::OPEN_PART>(wcur, ring, G::AHEAD, tid);
+    }
 
     float4 bv[kNT];  // folded bias of this lane's output channels (current layer)
     load_bias<G>(bv, N, 0, wn, lane);
 
     // per-lane bases: fragment reads (row of position tile m + k-group chunk),
     // epilogue writes (row + k-group's 8-byte half chunk), weight fragments
+    // (edge-row tiles: tile m is board row m, one lane base + m x 10 rows, so
+    // every tile's offset folds into the LDS instructions' immediates)
     int rd[kMT], wr[kMT];
+    const int erow0 = G::EDGE ? edge_tile_row<G>(wm, 0, lane & 15) * G::RP : 0;
 #pragma unroll
     for (int m = 0; m < kMT; ++m) {
-        const int rowb = (G::EDGE ? edge_tile_row<G>(wm, m, lane & 15)
-                                  : wm * G::BROWS + G::prow(kTilePos.p[16 * m + (lane & 15)])) *
-                         G::RP;
+        const int rowb = G::EDGE ? erow0 + m * 10 * G::RP
+                                 : (wm * G::BROWS + G::prow(kTilePos.p[16 * m + (lane & 15)])) * G::RP;
         rd[m] = rowb + kgroup_chunk(kg) * 16;
         wr[m] = rowb;
     }
     const int wl = (wn * kNT * 64 + lane) * 16;
+
+    // DIRECT: K-step g's weight fragments live in wq[g % WQ]; the K-step whose
+    // MFMAs a step issues loads K-step g + WQ - 1 (the stream pointer wgp is
+    // uniform, the lane's fragment offset wl). The packed weights run on
+    // through the first conv's pad step and every layer, so g counts K-steps
+    // over the whole network (tower layers start at g = WOFF mod WQ); loads
+    // past the last K-step read the zero pad behind the weights.
+    constexpr int WQ = G::DIRECT ? G::WQ : 1;
+    constexpr int WOFF = ksteps_first(C) % WQ;
+    u32x4_t wq[WQ][kNT];
+    const unsigned char* wgp = wsrc;
+    auto wload = [&](auto SLOT) {
+        constexpr int q = decltype(SLOT)::value % WQ;
+#pragma unroll
+        for (int n = 0; n < kNT; ++n) wq[q][n] = *reinterpret_cast<const u32x4_t*>(wgp + wl + n * 1024);
+        wgp += G::KSTEP_BYTES;
+    };
+    if constexpr (G::DIRECT) static_for<WQ - 1>([&](auto I) { wload(I); });
 
     // ---------------- zero border rows; input planes -> channels 0..31 ------
     // border cells per board: bordered boards 10 top + 10 bottom + 16 side,
@@ -821,10 +857,10 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         }
     }
     // stage 0 and the input planes must be visible (bias loads are older than the DMAs)
-    wait_vm<G::VM_LAYER>();
+    if constexpr (!G::DIRECT) wait_vm<G::VM_LAYER>();
     lds_barrier();
     // the first conv's K-step 0 (tap 0, dy = -1: edge-row geometries skip tile 0)
-    load_wfrags(fa, ring, wl);
+    if constexpr (!G::DIRECT) load_wfrags(fa, ring, wl);
 #pragma unroll
     for (int m = kWide ? 1 : 0; m < kMT; ++m)
         fa.x[m] = *reinterpret_cast<const u32x4_t*>(act + first_kstep_offset<C>(0) + rd[m]);
@@ -868,9 +904,10 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         // tiles [mlo, mhi) of cur (edge-row geometries leave out the border
         // tiles of the first conv). xoff: uniform byte offset of the next
         // K-step's activation rows/channels
-        auto step = [&](auto KIS, auto TILES, const Frags<kNT, kMT>& cur, Frags<kNT, kMT>& nxt, int xoff) {
+        auto step = [&](auto KIS, auto TILES, auto GI, const Frags<kNT, kMT>& cur, Frags<kNT, kMT>& nxt, int xoff) {
             constexpr int kis = decltype(KIS)::value;
-            constexpr bool open = kis == 0;
+            constexpr int gi = decltype(GI)::value;  // cur's K-step (DIRECT: first conv only)
+            constexpr bool open = kis == 0 && !G::DIRECT;
             constexpr int tl = decltype(TILES)::value;
             constexpr int xlo = tl & 15, xhi = (tl >> 4) & 15, mlo = (tl >> 8) & 15, mhi = (tl >> 12) & 15;
             // keep each step's MFMAs (on cur) with the fragment reads they hide:
@@ -899,22 +936,34 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 wcur += G::STAGE;
                 issue_stage_dma<G, G::OPEN_PART>(wcur, ring, sp, tid);
                 slot = slot == G::RING - 1 ? 0 : slot + 1;
-            } else if constexpr (G::SPLIT_DMA) {
+            } else if constexpr (G::SPLIT_DMA && !G::DIRECT) {
                 // the rest of the newest stage (its slot was freed by the barrier
                 // that opened the current stage)
                 int sa = slot + G::AHEAD;
                 sa = sa >= G::RING ? sa - G::RING : sa;
                 issue_stage_dma<G, G::MID_PART>(wcur, ring, sa, tid);
             }
-            load_wfrags(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
+            if constexpr (G::DIRECT) wload(std::integral_constant<int, gi + WQ - 1>{});
+            else load_wfrags(nxt, ring + slot * G::STAGE + kis * G::KSTEP_BYTES, wl);
 #pragma unroll
             for (int n = 0; n < kNT; ++n)
 #pragma unroll
-                for (int m = mlo; m < mhi; ++m) acc[n][m] = mfma<DT>(cur.w[n], cur.x[m], acc[n][m]);
+                for (int m = mlo; m < mhi; ++m) {
+                    if constexpr (G::DIRECT) acc[n][m] = mfma<DT>(wq[gi % WQ][n], cur.x[m], acc[n][m]);
+                    else acc[n][m] = mfma<DT>(cur.w[n], cur.x[m], acc[n][m]);
+                }
             // fine interleave of the step's fragment reads with its MFMAs (one
             // read, then a share of the MFMAs; +2.5 %): a stage-opening step has
             // only its weight reads after the barrier
-            if constexpr (kMT != 4) {
+            if constexpr (G::DIRECT) {
+                constexpr int nds = xhi - xlo;
+                constexpr int nm = kNT * (mhi - mlo);
+                static_for<nds>([&](auto I) {
+                    constexpr int i = decltype(I)::value;
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, (i + 1) * nm / nds - i * nm / nds, 0);
+                });
+            } else if constexpr (kMT != 4) {
                 constexpr int nds = open ? kNT : kNT + (xhi - xlo);
                 constexpr int nm = kNT * (mhi - mlo);
                 static_for<nds>([&](auto I) {
@@ -944,17 +993,22 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             static_for<nk - 1>([&](auto II) {
                 constexpr int i1 = decltype(II)::value + 1;  // the K-step this step loads
                 constexpr int tl = (tiles(i1) & 0xFF) | (tiles(i1 - 1) & 0xFF00);
+                using GI = std::integral_constant<int, i1 - 1>;
                 if constexpr (i1 % 2 == 1) step(std::integral_constant<int, i1 % G::KS>{},
-                                                std::integral_constant<int, tl>{}, fa, fb, first_kstep_offset<C>(i1));
-                else step(std::integral_constant<int, i1 % G::KS>{}, std::integral_constant<int, tl>{}, fb, fa,
+                                                std::integral_constant<int, tl>{}, GI{}, fa, fb, first_kstep_offset<C>(i1));
+                else step(std::integral_constant<int, i1 % G::KS>{}, std::integral_constant<int, tl>{}, GI{}, fb, fa,
                           first_kstep_offset<C>(i1));
             });
             constexpr int ml = tiles(nk - 1) >> 8 & 15, mh = tiles(nk - 1) >> 12 & 15;
             const Frags<kNT, kMT>& last = (nk - 1) % 2 == 1 ? fb : fa;
+            if constexpr (G::DIRECT) wload(std::integral_constant<int, nk - 1 + WQ - 1>{});
 #pragma unroll
             for (int n = 0; n < kNT; ++n)
 #pragma unroll
-                for (int m = ml; m < mh; ++m) acc[n][m] = mfma<DT>(last.w[n], last.x[m], acc[n][m]);
+                for (int m = ml; m < mh; ++m) {
+                    if constexpr (G::DIRECT) acc[n][m] = mfma<DT>(wq[(nk - 1) % WQ][n], last.x[m], acc[n][m]);
+                    else acc[n][m] = mfma<DT>(last.w[n], last.x[m], acc[n][m]);
+                }
         } else if constexpr (kWide) {
             constexpr int KPT = C / 32;
             static_assert(kNT == 2 && kMT == 8 && KPT % 2 == 0 && (3 * KPT) % G::KS == 0, "wide geometry");
@@ -968,7 +1022,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             auto wstep = [&](auto JJ, const Frags<kNT, kMT>& wc, Frags<kNT, kMT>& wn, int sbn) {
                 constexpr int J = decltype(JJ)::value;
                 constexpr int Jn = (J + 1) % NJ;
-                constexpr bool open = Jn % G::KS == 0;
+                constexpr bool open = Jn % G::KS == 0 && !G::DIRECT;
                 constexpr int dy = wide_dy(J), cbn = wide_cb(Jn), nnew = __builtin_popcount(wide_new(Jn));
                 constexpr int mlo = dy < 0 ? 1 : 0, mhi = dy > 0 ? 7 : 8;
                 auto& Wc = [&]() -> u32x4_t(&)[9] {
@@ -991,17 +1045,21 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     wcur += G::STAGE;
                     issue_stage_dma<G, G::OPEN_PART>(wcur, ring, sp, tid);
                     slot = slot == G::RING - 1 ? 0 : slot + 1;
-                } else if constexpr (G::SPLIT_DMA) {
+                } else if constexpr (G::SPLIT_DMA && !G::DIRECT) {
                     int sa = slot + G::AHEAD;
                     sa = sa >= G::RING ? sa - G::RING : sa;
                     issue_stage_dma<G, G::MID_PART>(wcur, ring, sa, tid);
                 }
-                load_wfrags(wn, ring + slot * G::STAGE + (Jn % G::KS) * G::KSTEP_BYTES, wl);
+                if constexpr (G::DIRECT) wload(std::integral_constant<int, WOFF + J + WQ - 1>{});
+                else load_wfrags(wn, ring + slot * G::STAGE + (Jn % G::KS) * G::KSTEP_BYTES, wl);
 #pragma unroll
                 for (int n = 0; n < kNT; ++n)
 #pragma unroll
-                    for (int m = mlo; m < mhi; ++m) acc[n][m] = mfma<DT>(wc.w[n], Wc[m + 1 + dy], acc[n][m]);
-                constexpr int nds = open ? kNT : kNT + nnew;
+                    for (int m = mlo; m < mhi; ++m) {
+                        if constexpr (G::DIRECT) acc[n][m] = mfma<DT>(wq[(WOFF + J) % WQ][n], Wc[m + 1 + dy], acc[n][m]);
+                        else acc[n][m] = mfma<DT>(wc.w[n], Wc[m + 1 + dy], acc[n][m]);
+                    }
+                constexpr int nds = G::DIRECT ? nnew : (open ? kNT : kNT + nnew);
                 constexpr int nm = kNT * (mhi - mlo);
                 static_for<nds>([&](auto I) {
                     constexpr int i = decltype(I)::value;
@@ -1020,10 +1078,14 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 });
                 if constexpr (lastdx) {
                     // the layer's last K-step = (last block, dy +1) in fb / win1
+                    if constexpr (G::DIRECT) wload(std::integral_constant<int, WOFF + NJ - 1 + WQ - 1>{});
 #pragma unroll
                     for (int n = 0; n < kNT; ++n)
 #pragma unroll
-                        for (int m = 0; m < 7; ++m) acc[n][m] = mfma<DT>(fb.w[n], win1[m + 2], acc[n][m]);
+                        for (int m = 0; m < 7; ++m) {
+                            if constexpr (G::DIRECT) acc[n][m] = mfma<DT>(wq[(WOFF + NJ - 1) % WQ][n], win1[m + 2], acc[n][m]);
+                            else acc[n][m] = mfma<DT>(fb.w[n], win1[m + 2], acc[n][m]);
+                        }
                 }
             };
 #pragma nounroll
@@ -1042,8 +1104,8 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     constexpr int J = decltype(JJ)::value;
                     using KIS = std::integral_constant<int, (J + 1) % G::KS>;
                     const int xo = J == NJ - 1 ? xoff_of(dxi + 1, 0) : xoff_of(dxi, J + 1);
-                    if constexpr (J % 2 == 0) step(KIS{}, AllTiles{}, fa, fb, xo);
-                    else step(KIS{}, AllTiles{}, fb, fa, xo);
+                    if constexpr (J % 2 == 0) step(KIS{}, AllTiles{}, std::integral_constant<int, 0>{}, fa, fb, xo);
+                    else step(KIS{}, AllTiles{}, std::integral_constant<int, 0>{}, fb, fa, xo);
                 });
             };
 #pragma nounroll
@@ -1060,8 +1122,10 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         OAMD_EP_MARK(0);
         lds_barrier();  // every wave is done reading this layer's input and its last stage
         OAMD_EP_MARK(1);
-        wcur += G::STAGE;
-        issue_stage_dma<G, G::OPEN_PART>(wcur, ring, (slot + G::AHEAD + 1) % G::RING, tid);
+        if constexpr (!G::DIRECT) {
+            wcur += G::STAGE;
+            issue_stage_dma<G, G::OPEN_PART>(wcur, ring, (slot + G::AHEAD + 1) % G::RING, tid);
+        }
         if constexpr (kNT == 2) {
             // the wave's two channel tiles hold 8 contiguous channels per lane
             // (out_chan): one 16-byte store (and skip read) per position tile
@@ -1093,10 +1157,10 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         OAMD_EP_MARK(2);
         if (more) {
             // the next layer's first stage has landed (later may fly)
-            wait_vm<G::VM_LAYER>();
+            if constexpr (!G::DIRECT) wait_vm<G::VM_LAYER>();
             lds_barrier();  // ... and this layer's output is complete
             if constexpr (kWide) {
-                load_wfrags(fa, ring + slot * G::STAGE, wl);
+                if constexpr (!G::DIRECT) load_wfrags(fa, ring + slot * G::STAGE, wl);
 #pragma unroll
                 for (int i = 1; i < 8; ++i) win0[i] = *reinterpret_cast<const u32x4_t*>(act + sb0 + i * 10 * G::RP);
             } else {

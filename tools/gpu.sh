@@ -14,6 +14,7 @@
 #   variants NAME [VAR=val ...]    nn timing of every prebuilt abv/<v>/liboamd.so (tools/variants.sh
 #                                  builds them here), ROUNDS interleaved sweeps, outputs compared bit
 #                                  for bit with the first variant's
+#   stamps NAME VARIANT [VAR=val]  tools/nn_stamps.py with abv/VARIANT (built with -DOAMD_STAMPS)
 #   benchvar NAME [bench args]     bench line of every prebuilt variant, ROUNDS interleaved sweeps
 # Every step runs under its own time limit; the first failing step ends the run
 # (no retries). Summaries: python tools/prof_summary.py (in the build container).
@@ -62,6 +63,11 @@ run_recipe() {
         done
       done
       restore_lib ;;
+    stamps) local n=$1 v=$2; shift 2  # tools/nn_stamps.py on a -DOAMD_STAMPS variant
+      cp $PKG/liboamd.so /tmp/liboamd.so.orig
+      cp abv/$v/liboamd.so $PKG/liboamd.so
+      step 300 "$OUT/stamps_$n.log" env "$@" python tools/nn_stamps.py; local rc=$?
+      restore_lib; return $rc ;;
     benchvar) local n=$1; shift
       cp $PKG/liboamd.so /tmp/liboamd.so.orig
       for r in $(seq ${ROUNDS:-2}); do
