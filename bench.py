@@ -12,7 +12,11 @@ GPUs without the explicit gloo rehearsal (OAMD_BENCH_BACKEND=gloo), fails.
 A step is one self-play move of every game on the GPU: a full 800-simulation
 search (25 steps of select -> fused ResNet -> expand/backup for T=2 x B=16
 leaves per game) followed by the on-device move choice, 8-fold target emission
-and move application (finished games restart from a random opening).
+and move application (finished games restart from a random opening). The K
+timed steps are one multi-move call (BatchedMCTS.selfplay_steps: per game the
+same kernels in the same order as K search + selfplay_move pairs; each
+pipeline group chains its moves on its own stream); --per-move-calls times K
+call pairs instead.
 Synthetic data: random-init AlphaZeroNet weights of the 128x10b architecture
 (seeded), random openings of 0..8 plies.
 
@@ -275,6 +279,8 @@ def parse_args(argv: list[str]):
                     help="torch threads of the CPU baseline (0 = every CPU this process may use)")
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
+    ap.add_argument("--per-move-calls", action="store_true",
+                    help="one search + selfplay_move call pair per step instead of one multi-move call")
     ap.add_argument("--timing-every", type=int, default=5,
                     help="record the kernels' HIP events on every N-th timed search (1 = all; the event "
                          "packets add ~10 us per NN launch boundary to the searches they time)")
@@ -363,6 +369,18 @@ class EngineWorkload:
         self.b.search(self.net, sync=self.args.sync_search)  # enqueue only; the timed region syncs at its end
         self.b.selfplay_move(temperature_moves=12, opening_moves=8, emit_targets=True)
 
+    def steps(self, n: int) -> None:
+        """n steps: one multi-move self-play call (oamd_engine_selfplay_steps, the
+        same kernels per game as n x step(); each pipeline group's move and next
+        selection overlap the other group's ResNet launch), or n x step() with
+        --per-move-calls / --sync-search."""
+        if self.args.per_move_calls or self.args.sync_search:
+            for _ in range(n):
+                self.step()
+        else:
+            self.b.selfplay_steps(self.net, n, temperature_moves=12, opening_moves=8, emit_targets=True,
+                                  keep_all=False)
+
     def sync(self) -> None:
         torch.cuda.synchronize()
 
@@ -387,16 +405,21 @@ class EngineWorkload:
 def report(args, world: int, rank: int, backend: str, wl) -> None:
     L = args.threads * args.batch
     sims_per_search = L * ((args.sims + L - 1) // L)
-    for _ in range(args.warmup):
-        wl.step()
+    def steps(n: int) -> None:
+        if hasattr(wl, "steps"):
+            wl.steps(n)
+        else:
+            for _ in range(n):
+                wl.step()
+
+    steps(args.warmup)
     wl.sync()
     measuring = hasattr(wl, "start_measuring")
     if measuring:
         wl.start_measuring()
 
     def run():
-        for _ in range(args.steps):
-            wl.step()
+        steps(args.steps)
 
     dt_max = timed_max(world, run, wl.sync, "cuda" if backend == "nccl" else "cpu")
     m = wl.stop_measuring() if measuring else None
@@ -438,6 +461,8 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
             "ranks": ranks,
             "backend": (backend if world > 1 else "none"),
             "endgame_interleaving": "round-robin" if args.round_robin_endgames else "exact (reference)",
+            "calls": ("search + selfplay_move per step" if args.per_move_calls or args.sync_search
+                      else f"one selfplay_steps call for the {args.steps} timed steps"),
         },
     }
     if args.dry_run:

@@ -268,6 +268,17 @@ typedef struct oamd_selfplay_config {
 int oamd_engine_selfplay_move(oamd_engine *e, const oamd_selfplay_config *cfg,
                               int32_t *actions_dev, int32_t *finished_dev, float *features_dev,
                               float *policy_dev);
+/* n_moves self-play moves of every game with the native net: per move one
+ * oamd_engine_search + oamd_engine_selfplay_move, identical results, but each
+ * pipeline group chains its searches and moves on its own stream (no join
+ * between moves: a group's move and next selection overlap the other groups'
+ * ResNet launches). Enqueued only (stream order). per_move_outputs = 1: the
+ * output buffers hold n_moves consecutive slices of the per-move shapes above
+ * (move i at offset i x G rows); 0: every move overwrites the same slice.
+ * Replaces the reference's per-move loop train.py:404-452 (_self_play). */
+int oamd_engine_selfplay_steps(oamd_engine *e, oamd_net *net, const oamd_selfplay_config *cfg,
+                               int32_t n_moves, int32_t per_move_outputs, int32_t *actions_dev,
+                               int32_t *finished_dev, float *features_dev, float *policy_dev);
 /* Reset every game to a random opening. */
 int oamd_engine_random_openings(oamd_engine *e, int32_t max_moves, uint64_t seed);
 /* The random-stream key of a game (DESIGN.md "Random streams"). */

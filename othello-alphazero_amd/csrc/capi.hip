@@ -878,23 +878,155 @@ int oamd_engine_tree_timing(const oamd_engine* ce, float* select_ms, float* back
     return OAMD_OK;
 }
 
-int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* evals) {
+// Pipeline groups of a native search: the games split into K contiguous
+// groups, each on its own stream, so one group's tree kernels (latency-bound,
+// a wave per game) run while another group's ResNet launch owns the MFMA
+// units. Games are independent, so the results are identical for every K.
+struct GroupPlan {
+    int K = 1;
+    hipStream_t st[kMaxPipeline] = {};
+    int g0[kMaxPipeline] = {}, ng[kMaxPipeline] = {};
+};
+
+static int native_search_checks(const oamd_engine* e, const oamd_net* net) {
     if (!net || !net->loaded) return fail(OAMD_INVALID_ARGUMENT, "native net not loaded");
     if (net->device != e->device) return fail(OAMD_INVALID_ARGUMENT, "net and engine on different devices");
     if (net->desc.in_channels != 1 + 2 * e->cfg.history_size)
         return fail(OAMD_INVALID_ARGUMENT, "net in_channels != 1 + 2 * history_size");
+    return OAMD_OK;
+}
+
+static GroupPlan plan_groups(oamd_engine* e) {
+    GroupPlan P;
+    int K = e->pipeline > 0 ? e->pipeline : (e->G >= 64 ? 2 : 1);
+    if (K > e->G) K = e->G;
+    if (K > kMaxPipeline) K = kMaxPipeline;
+    P.K = K;
+    for (int k = 0; k < K; ++k) {
+        P.g0[k] = (int)((int64_t)e->G * k / K);
+        P.ng[k] = (int)((int64_t)e->G * (k + 1) / K) - P.g0[k];
+        P.st[k] = K == 1 ? e->stream : e->pipe_stream[k];
+    }
+    return P;
+}
+
+// Sampled timing of one search: claim the current event pool (every
+// timing_stride-th search), sized for NB blocks per round.
+static int timing_begin(oamd_engine* e, int steps, int NB, bool* timed) {
+    *timed = e->timing && (e->search_count++ % e->timing_stride) == 0;
+    if (!*timed) return OAMD_OK;
+    const int pool = e->ev_cur;
+    if (int rc = e->resolve_timing(pool)) return rc;
+    while ((int)e->ev[pool].size() < kEvPerBlock * (steps + 1) * NB) {
+        hipEvent_t x;
+        HIPCHK(hipEventCreate(&x));
+        e->ev[pool].push_back(x);
+    }
+    return OAMD_OK;
+}
+
+static void timing_end(oamd_engine* e, int steps, int NB, bool split, const GroupPlan& P) {
+    const int pool = e->ev_cur;
+    e->ev_blocks[pool] = (steps + 1) * NB;
+    e->ev_final[pool] = steps * NB;
+    e->ev_K[pool] = NB;
+    e->ev_nn_groups[pool] = NB;
+    int64_t nl = 0, rows = 0;
+    if (split) {
+        nl = e->cfg.num_threads;
+        rows = e->L();
+    }
+    for (int k = 0; !split && k < e->ev_nn_groups[pool]; ++k) {
+        const int grows = P.ng[k] * e->L(), cb = e->nn_batch > 0 ? e->nn_batch : grows;
+        nl += (grows + cb - 1) / cb;
+        rows += grows;
+    }
+    e->ev_launches[pool] = (int64_t)steps * nl;
+    e->ev_rows[pool] = (int64_t)steps * rows;
+    e->ev_cur ^= 1;
+}
+
+// The rounds of one native search over the groups of P, enqueued on the group
+// streams (already forked from the engine stream). chained: the groups'
+// streams carry on from a previous search of the same call (a multi-move
+// self-play call), so its first NN launch also waits for the NN token.
+static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPlan& P, int steps, bool timed,
+                                bool chained) {
+    const EngineView E = e->view();
+    const int K = P.K, L = e->L();
+    const int T = e->cfg.num_threads, B = e->cfg.batch_size;
+    const int pool = e->ev_cur;
+    const int nch = e->nn_chains < K ? e->nn_chains : K;
+    // rounds 0..steps (k_tree): round s backs up batch s-1 and selects batch s,
+    // thread by thread; the NN evaluates batch s between rounds s and s+1
+    for (int s = 0; s <= steps; ++s) {
+        for (int k = 0; k < K; ++k) {
+            const size_t r0 = (size_t)P.g0[k] * L;
+            hipStream_t sk = P.st[k];
+            hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
+            if (ev) HIPCHK(hipEventRecord(ev[0], sk));
+            // evaluation list of group k: round s fills counter s % 2 and zeroes
+            // the other one (which round s-1's launch, done by now, read); the
+            // final round zeroes counter 0 for the next search's round 0
+            int* cnt = e->rowcount + 2 * k;
+            launch_tree(E, sk, s > 0, s < steps, T, B, P.g0[k], P.ng[k], 0, -1, s < steps ? cnt + (s & 1) : nullptr,
+                        s < steps ? cnt + ((s + 1) & 1) : cnt, s == 0);
+            if (ev) HIPCHK(hipEventRecord(ev[1], sk));
+            if (s == steps) continue;
+            // the groups' NN launches run one after another (OAMD_NN_ORDER)
+            hipStream_t ns = sk;
+            if (K > 1 && OAMD_NN_ORDER == 2) {
+                ns = e->nn_stream;
+                HIPCHK(hipEventRecord(e->sel_ev[k], sk));
+                HIPCHK(hipStreamWaitEvent(ns, e->sel_ev[k], 0));
+            } else if (K > 1 && OAMD_NN_ORDER == 1 && (s > 0 || k >= nch || chained)) {
+                HIPCHK(hipStreamWaitEvent(sk, e->nn_token[k % nch], 0));
+            }
+            if (ev) HIPCHK(hipEventRecord(ev[2], ns));
+            const int grows = P.ng[k] * L;
+            const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
+            for (int r = 0; r < grows; r += cb)
+                launch_resnet_packed(N, E.feat, E.FW, E.H, std::min(cb, grows - r), E.policy, E.value, ns,
+                                     E.rowlist + r0 + r, cnt + (s & 1), r);
+            if (ev) HIPCHK(hipEventRecord(ev[3], ns));
+            if (K > 1 && OAMD_NN_ORDER == 2) {
+                HIPCHK(hipEventRecord(e->nn_ev[k], ns));
+                HIPCHK(hipStreamWaitEvent(sk, e->nn_ev[k], 0));
+            } else if (K > 1 && OAMD_NN_ORDER == 1) {
+                HIPCHK(hipEventRecord(e->nn_token[k % nch], sk));
+            }
+        }
+    }
+    return OAMD_OK;
+}
+
+static int fork_groups(oamd_engine* e, const GroupPlan& P) {
+    if (P.K > 1) {  // fork from the caller's stream
+        HIPCHK(hipEventRecord(e->fork_ev, e->stream));
+        for (int k = 0; k < P.K; ++k) HIPCHK(hipStreamWaitEvent(P.st[k], e->fork_ev, 0));
+    }
+    return OAMD_OK;
+}
+
+static int join_groups(oamd_engine* e, const GroupPlan& P) {
+    if (P.K > 1) {  // join back into the caller's stream
+        for (int k = 0; k < P.K; ++k) {
+            HIPCHK(hipEventRecord(e->join_ev[k], P.st[k]));
+            HIPCHK(hipStreamWaitEvent(e->stream, e->join_ev[k], 0));
+        }
+    }
+    return OAMD_OK;
+}
+
+int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* evals) {
+    if (int rc = native_search_checks(e, net)) return rc;
     DeviceGuard dg(e->device);
     const int L = e->L();
     const int steps = (e->cfg.num_simulations + L - 1) / L;
     const EngineView E = e->view();
     const NetView N = net->view();
-    // Pipeline groups: the games are split into K contiguous groups, each on its
-    // own stream, so one group's tree kernels (latency-bound, a wave per game)
-    // run while another group's ResNet launch owns the MFMA units. Games are
-    // independent, so the results are identical for every K.
-    int K = e->pipeline > 0 ? e->pipeline : (e->G >= 64 ? 2 : 1);
-    if (K > e->G) K = e->G;
-    if (K > kMaxPipeline) K = kMaxPipeline;
+    GroupPlan P = plan_groups(e);
+    const int K = P.K;
     const int T = e->cfg.num_threads, B = e->cfg.batch_size;
     // One game with T > 1 virtual threads (the drop-in MCTS, latency mode):
     // the tree kernel runs thread by thread on the engine stream, and thread
@@ -907,34 +1039,13 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     const int NB = split ? T : K;  // timing blocks per round
     int rc = split ? e->ensure_streams(2, T) : e->ensure_streams(K, K);
     if (rc) return rc;
+    if (!split) P = plan_groups(e);  // the group streams exist now
     if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
-    // sampled timing: every timing_stride-th search records its events
-    const bool timed = e->timing && (e->search_count++ % e->timing_stride) == 0;
-    // timing: per (round, group) kEvPerBlock events: tree begin/end, NN
+    // sampled timing: per (round, group) kEvPerBlock events: tree begin/end, NN
     // begin/end (on the NN stream, after its waits; not in the final round)
+    bool timed = false;
+    if ((rc = timing_begin(e, steps, NB, &timed))) return rc;
     const int pool = e->ev_cur;
-    if (timed) {
-        if ((rc = e->resolve_timing(pool))) return rc;
-        while ((int)e->ev[pool].size() < kEvPerBlock * (steps + 1) * NB) {
-            hipEvent_t x;
-            HIPCHK(hipEventCreate(&x));
-            e->ev[pool].push_back(x);
-        }
-    }
-    hipStream_t st[kMaxPipeline];
-    int g0[kMaxPipeline], ng[kMaxPipeline];
-    for (int k = 0; k < K; ++k) {
-        g0[k] = (int)((int64_t)e->G * k / K);
-        ng[k] = (int)((int64_t)e->G * (k + 1) / K) - g0[k];
-        st[k] = K == 1 ? e->stream : e->pipe_stream[k];
-    }
-    if (K > 1) {  // fork from the caller's stream
-        HIPCHK(hipEventRecord(e->fork_ev, e->stream));
-        for (int k = 0; k < K; ++k) HIPCHK(hipStreamWaitEvent(st[k], e->fork_ev, 0));
-    }
-    // rounds 0..steps (k_tree): round s backs up batch s-1 and selects batch s,
-    // thread by thread; the NN evaluates batch s between rounds s and s+1
-    const int nch = e->nn_chains < K ? e->nn_chains : K;
     for (int s = 0; split && s <= steps; ++s) {
         for (int t = 0; t < T; ++t) {
             hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * T + t)] : nullptr;
@@ -953,70 +1064,13 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             HIPCHK(hipEventRecord(e->nn_ev[t], ns));
         }
     }
-    for (int s = 0; !split && s <= steps; ++s) {
-        for (int k = 0; k < K; ++k) {
-            const size_t r0 = (size_t)g0[k] * L;
-            hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
-            if (ev) HIPCHK(hipEventRecord(ev[0], st[k]));
-            // evaluation list of group k: round s fills counter s % 2 and zeroes
-            // the other one (which round s-1's launch, done by now, read); the
-            // final round zeroes counter 0 for the next search's round 0
-            int* cnt = e->rowcount + 2 * k;
-            launch_tree(E, st[k], s > 0, s < steps, T, B, g0[k], ng[k], 0, -1, s < steps ? cnt + (s & 1) : nullptr,
-                        s < steps ? cnt + ((s + 1) & 1) : cnt, s == 0);
-            if (ev) HIPCHK(hipEventRecord(ev[1], st[k]));
-            if (s == steps) continue;
-            // the groups' NN launches run one after another (OAMD_NN_ORDER)
-            hipStream_t ns = st[k];
-            if (K > 1 && OAMD_NN_ORDER == 2) {
-                ns = e->nn_stream;
-                HIPCHK(hipEventRecord(e->sel_ev[k], st[k]));
-                HIPCHK(hipStreamWaitEvent(ns, e->sel_ev[k], 0));
-            } else if (K > 1 && OAMD_NN_ORDER == 1 && (s > 0 || k >= nch)) {
-                HIPCHK(hipStreamWaitEvent(st[k], e->nn_token[k % nch], 0));
-            }
-            const bool nn_timed = ev != nullptr;
-            if (nn_timed) HIPCHK(hipEventRecord(ev[2], ns));
-            const int grows = ng[k] * L;
-            const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
-            for (int r = 0; r < grows; r += cb)
-                launch_resnet_packed(N, E.feat, E.FW, E.H, std::min(cb, grows - r), E.policy, E.value, ns,
-                                     E.rowlist + r0 + r, cnt + (s & 1), r);
-            if (nn_timed) HIPCHK(hipEventRecord(ev[3], ns));
-            if (K > 1 && OAMD_NN_ORDER == 2) {
-                HIPCHK(hipEventRecord(e->nn_ev[k], ns));
-                HIPCHK(hipStreamWaitEvent(st[k], e->nn_ev[k], 0));
-            } else if (K > 1 && OAMD_NN_ORDER == 1) {
-                HIPCHK(hipEventRecord(e->nn_token[k % nch], st[k]));
-            }
-        }
+    if (!split) {
+        if ((rc = fork_groups(e, P))) return rc;
+        if ((rc = enqueue_group_rounds(e, N, P, steps, timed, false))) return rc;
     }
     LAUNCHCHK();
-    if (K > 1) {  // join back into the caller's stream
-        for (int k = 0; k < K; ++k) {
-            HIPCHK(hipEventRecord(e->join_ev[k], st[k]));
-            HIPCHK(hipStreamWaitEvent(e->stream, e->join_ev[k], 0));
-        }
-    }
-    if (timed) {
-        e->ev_blocks[pool] = (steps + 1) * NB;
-        e->ev_final[pool] = steps * NB;
-        e->ev_K[pool] = NB;
-        e->ev_nn_groups[pool] = NB;
-        int64_t nl = 0, rows = 0;
-        if (split) {
-            nl = T;
-            rows = L;
-        }
-        for (int k = 0; !split && k < e->ev_nn_groups[pool]; ++k) {
-            const int grows = ng[k] * L, cb = e->nn_batch > 0 ? e->nn_batch : grows;
-            nl += (grows + cb - 1) / cb;
-            rows += grows;
-        }
-        e->ev_launches[pool] = (int64_t)steps * nl;
-        e->ev_rows[pool] = (int64_t)steps * rows;
-        e->ev_cur ^= 1;
-    }
+    if (!split && (rc = join_groups(e, P))) return rc;
+    if (timed) timing_end(e, steps, NB, split, P);
     // without counters requested the search is left in flight (stream order)
     if (sims || evals) {
         unsigned long long c[2] = {0, 0};
@@ -1168,8 +1222,62 @@ int oamd_engine_selfplay_move(oamd_engine* e, const oamd_selfplay_config* cfg, i
         return fail(OAMD_INVALID_ARGUMENT, "emit_targets needs features and policy buffers");
     SelfplayParams sp{cfg->temperature_moves, cfg->temperature, cfg->opening_moves, cfg->emit_targets};
     DeviceGuard dg(e->device);
-    launch_selfplay_move(e->view(), sp, actions_dev, finished_dev, features_dev, policy_dev, e->stream);
+    launch_selfplay_move(e->view(), sp, 0, e->G, actions_dev, finished_dev, features_dev, policy_dev, e->stream);
     LAUNCHCHK();
+    return OAMD_OK;
+}
+
+int oamd_engine_selfplay_steps(oamd_engine* e, oamd_net* net, const oamd_selfplay_config* cfg, int32_t n_moves,
+                               int32_t per_move_outputs, int32_t* actions_dev, int32_t* finished_dev,
+                               float* features_dev, float* policy_dev) {
+    if (n_moves < 0) return fail(OAMD_INVALID_ARGUMENT, "n_moves must be >= 0");
+    if (cfg->temperature_moves < 0 || !(cfg->temperature > 0.0f) || cfg->opening_moves < 0)
+        return fail(OAMD_INVALID_ARGUMENT, "bad self-play config");
+    if (cfg->emit_targets && (!features_dev || !policy_dev))
+        return fail(OAMD_INVALID_ARGUMENT, "emit_targets needs features and policy buffers");
+    if (int rc = native_search_checks(e, net)) return rc;
+    DeviceGuard dg(e->device);
+    const int G = e->G, C = 1 + 2 * e->cfg.history_size;
+    // move i's outputs: the i-th slice of per-move buffers, or the same G-game buffers every move
+    auto out = [&](int i, auto* p, int64_t per_game) { return p ? p + (per_move_outputs ? (int64_t)i * G * per_game : 0) : p; };
+    GroupPlan P = plan_groups(e);
+    const int T = e->cfg.num_threads;
+    const bool split = G == 1 && P.K == 1 && T > 1 && T <= kMaxPipeline && e->tree_split();
+    if (split || P.K == 1) {  // one stream: the plain sequence of calls
+        for (int i = 0; i < n_moves; ++i) {
+            if (int rc = oamd_engine_search(e, net, nullptr, nullptr)) return rc;
+            if (int rc = oamd_engine_selfplay_move(e, cfg, out(i, actions_dev, 1), out(i, finished_dev, 1),
+                                                   out(i, features_dev, 8 * C * 64), out(i, policy_dev, 8 * 65)))
+                return rc;
+        }
+        return OAMD_OK;
+    }
+    if (int rc = e->ensure_streams(P.K, P.K)) return rc;
+    P = plan_groups(e);
+    const int L = e->L();
+    const int steps = (e->cfg.num_simulations + L - 1) / L;
+    const EngineView E = e->view();
+    const NetView N = net->view();
+    SelfplayParams sp{cfg->temperature_moves, cfg->temperature, cfg->opening_moves, cfg->emit_targets};
+    // Each group runs its own chain of searches and moves on its stream: its
+    // move and the next search's first selection overlap the other groups'
+    // last ResNet launches instead of waiting for a join after every move.
+    // Per game the kernels and their order are those of search + move calls.
+    int rc = fork_groups(e, P);
+    for (int i = 0; !rc && i < n_moves; ++i) {
+        bool timed = false;
+        if ((rc = timing_begin(e, steps, P.K, &timed))) break;
+        if ((rc = enqueue_group_rounds(e, N, P, steps, timed, i > 0))) break;
+        for (int k = 0; k < P.K; ++k)
+            launch_selfplay_move(E, sp, P.g0[k], P.ng[k], out(i, actions_dev, 1), out(i, finished_dev, 1),
+                                 out(i, features_dev, 8 * C * 64), out(i, policy_dev, 8 * 65), P.st[k]);
+        if (timed) timing_end(e, steps, P.K, false, P);
+    }
+    if (rc) return rc;
+    LAUNCHCHK();
+    if ((rc = join_groups(e, P))) return rc;
+    e->step_phase = 0;
+    e->steps_left = 0;
     return OAMD_OK;
 }
 

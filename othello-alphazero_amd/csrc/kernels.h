@@ -38,7 +38,7 @@ void launch_apply_one(const EngineView& E, int g, int action, hipStream_t s);
 void launch_root_stats(const EngineView& E, int game_begin, int n_games, oamd_root_info* info,
                        int32_t* visits, float* q, int by_action, hipStream_t s);
 void launch_self_play_data(const EngineView& E, int g, float* feat, float* pol, hipStream_t s);
-void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int32_t* actions,
+void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int g0, int ng, int32_t* actions,
                           int32_t* finished, float* feat, float* pol, hipStream_t s);
 void launch_random_openings(const EngineView& E, int max_moves, uint64_t seed, hipStream_t s);
 void launch_status(const EngineView& E, int32_t* out, hipStream_t s);

@@ -644,6 +644,15 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
                                                  reinterpret_cast<int32_t*>(finished), reinterpret_cast<float*>(feat),
                                                  reinterpret_cast<float*>(pol)));
              })
+        .def("selfplay_steps",
+             [](Engine& e, uintptr_t net, int n_moves, int temperature_moves, float temperature, int opening_moves,
+                bool emit, bool per_move_outputs, uintptr_t actions, uintptr_t finished, uintptr_t feat, uintptr_t pol) {
+                 oamd_selfplay_config c{temperature_moves, temperature, opening_moves, emit ? 1 : 0};
+                 check(oamd_engine_selfplay_steps(e.h, reinterpret_cast<oamd_net*>(net), &c, n_moves,
+                                                  per_move_outputs ? 1 : 0, reinterpret_cast<int32_t*>(actions),
+                                                  reinterpret_cast<int32_t*>(finished), reinterpret_cast<float*>(feat),
+                                                  reinterpret_cast<float*>(pol)));
+             })
         .def("random_openings",
              [](Engine& e, int max_moves, uint64_t seed) { check(oamd_engine_random_openings(e.h, max_moves, seed)); })
         .def("game_key",

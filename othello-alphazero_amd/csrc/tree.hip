@@ -812,10 +812,10 @@ __global__ void k_random_openings(EngineView E, int max_moves, uint64_t seed) {
 
 constexpr int kFinNoTargets = 4, kFinOverflow = 8;
 
-__global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayParams sp,
+__global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayParams sp, int g0,
                                                       int32_t* actions, int32_t* finished,
                                                       float* feat_out, float* pol_out) {
-    const int g = blockIdx.x;
+    const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     GameState* gs = E.games + g;
     if (!(gs->flags & kActive)) {
@@ -979,9 +979,10 @@ void launch_root_stats(const EngineView& E, int game_begin, int n_games, oamd_ro
 void launch_self_play_data(const EngineView& E, int g, float* feat, float* pol, hipStream_t s) {
     hipLaunchKernelGGL(k_self_play_data, dim3(1), dim3(512), 0, s, E, g, feat, pol);
 }
-void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int32_t* actions,
+void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int g0, int ng, int32_t* actions,
                           int32_t* finished, float* feat, float* pol, hipStream_t s) {
-    hipLaunchKernelGGL(k_selfplay_move, dim3(E.G), dim3(64), 0, s, E, sp, actions, finished, feat, pol);
+    if (ng > 0)
+        hipLaunchKernelGGL(k_selfplay_move, dim3(ng), dim3(64), 0, s, E, sp, g0, actions, finished, feat, pol);
 }
 void launch_status(const EngineView& E, int32_t* out, hipStream_t s) {
     hipLaunchKernelGGL(k_status, dim3(blocks_for(E.G, 64)), dim3(64), 0, s, E, out);

@@ -176,5 +176,36 @@ class BatchedMCTS:
             out["policy"] = self._targets_p
         return out
 
+    def selfplay_steps(self, neural_net, n_moves: int, temperature_moves: int = 12, temperature: float = 1.0,
+                       opening_moves: int = 0, emit_targets: bool = False,
+                       keep_all: bool = True) -> dict[str, torch.Tensor]:
+        """n_moves x (search(net) + selfplay_move(...)) in one enqueue, same results
+        move for move; each pipeline group chains its searches and moves on its own
+        stream, so the per-move join disappears (oamd_engine_selfplay_steps).
+        keep_all: outputs shaped (n_moves, G, ...); else only the last move's
+        (G, ...), every move writing the same buffers. Native net (or a module
+        search() would convert) only."""
+        self._stream()
+        net = resolve(neural_net, self.device.index, self.config.history_size)
+        if net is None:
+            raise TypeError("selfplay_steps needs a NativeNet (or an eval-mode AlphaZeroNet)")
+        n = max(0, int(n_moves))
+        lead = (n,) if keep_all else ()
+        actions = torch.empty(lead + (self.num_games,), dtype=torch.int32, device=self.device)
+        finished = torch.empty_like(actions)
+        feat = pol = None
+        if emit_targets:
+            feat = torch.empty(lead + (self.num_games, 8, self._C, 8, 8), dtype=torch.float32, device=self.device)
+            pol = torch.empty(lead + (self.num_games, 8, 65), dtype=torch.float32, device=self.device)
+        self.engine.selfplay_steps(net.handle, n, temperature_moves, temperature, opening_moves, emit_targets,
+                                   keep_all, actions.data_ptr(), finished.data_ptr(),
+                                   feat.data_ptr() if feat is not None else 0,
+                                   pol.data_ptr() if pol is not None else 0)
+        out = {"actions": actions, "finished": finished}
+        if emit_targets:
+            out["features"] = feat
+            out["policy"] = pol
+        return out
+
 
 __all__ = ["BatchedMCTS", "NativeNet"]

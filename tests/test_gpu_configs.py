@@ -228,3 +228,47 @@ def test_evaluation_lists_through_endgames(om, exact):
                     f"64 games x 75 moves: terminal-leaf share {share:.3f}, "
                     "native (lists, eval batch 0 / 384) == callback")
     assert share > 0.02  # the endgames were reached
+
+
+@pytest.mark.parametrize("G,pipeline", [(256, 0), (96, 3), (8, 0)])
+def test_selfplay_steps_equal_move_by_move(om, G, pipeline):
+    """oamd_engine_selfplay_steps (each pipeline group chains its searches and
+    moves on its own stream) == n x (search + selfplay_move): actions, finish
+    codes, 8-fold targets and the trees after the last move, bit for bit;
+    G=8 runs one group (the plain call sequence)."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(31, 9, 128, 2, 64), device=0)
+    n = 6
+
+    def engine():
+        b = om.BatchedMCTS(G, history_size=4, num_simulations=96, num_threads=2, batch_size=16, seed=G,
+                           node_capacity=1 << 15)
+        b.random_openings(55, seed=5)  # late openings: games end and restart inside the n moves
+        if pipeline:
+            b.engine.set_pipeline(pipeline)
+        return b
+
+    a = engine()
+    acts, fins, feats, pols = [], [], [], []
+    for _ in range(n):
+        a.search(net, sync=False)
+        o = a.selfplay_move(temperature_moves=12, opening_moves=4, emit_targets=True)
+        acts.append(o["actions"].clone())
+        fins.append(o["finished"].clone())
+        feats.append(o["features"].clone())
+        pols.append(o["policy"].clone())
+    b = engine()
+    o = b.selfplay_steps(net, n, temperature_moves=12, opening_moves=4, emit_targets=True)
+    torch.cuda.synchronize()
+    assert torch.equal(o["actions"], torch.stack(acts)) and torch.equal(o["finished"], torch.stack(fins))
+    assert torch.equal(o["features"], torch.stack(feats)) and torch.equal(o["policy"], torch.stack(pols))
+    va, qa = a.root_stats()
+    vb, qb = b.root_stats()
+    assert torch.equal(va, vb) and torch.equal(qa, qb)
+    restarts = int(((torch.stack(fins) & 3) != 0).sum())
+    assert a.engine.status() == (0, 0) and b.engine.status() == (0, 0)
+    if G >= 96:
+        assert restarts > 0
+    numerics.record(f"selfplay_steps G={G} pipeline={pipeline or 'auto'}",
+                    f"{n} moves identical to search + selfplay_move, {restarts} game ends")
