@@ -173,8 +173,9 @@ int oamd_engine_set_pipeline(oamd_engine *e, int32_t groups);
  * Results do not depend on it. */
 int oamd_engine_set_nn_batch(oamd_engine *e, int32_t rows);
 /* The pipeline groups' ResNet launches form `chains` chains (group k in chain
- * k % chains, 1..4, default 1): launches of one chain run one after another,
- * chains run concurrently. Results do not depend on it. */
+ * k % chains, 1..4, default 2): launches of one chain run one after another,
+ * chains run concurrently (the default lets the two groups' launches overlap
+ * at their ends). Results do not depend on it. */
 int oamd_engine_set_nn_chains(oamd_engine *e, int32_t chains);
 /* enable = 1 (default): the reference's thread interleaving exactly — a
  * virtual thread whose batch is all terminal backs it up without an NN round
@@ -290,6 +291,11 @@ int oamd_engine_game_key(oamd_engine *e, int32_t game, uint64_t *key_host);
  * (terminal leaves included; oamd_engine_work_counters gives the rows that
  * needed an evaluation). */
 int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches, int64_t *rows);
+/* The union of those NN launch intervals (ms some timed ResNet launch was
+ * running): equal to nn_ms when launches never overlap (one NN chain); with
+ * oamd_engine_set_nn_chains(e, n > 1) the groups' launches overlap and nn_ms
+ * counts the shared time once per launch. */
+int oamd_engine_nn_busy(const oamd_engine *e, float *busy_ms);
 /* Same for the tree kernel (k_tree, one launch per search round and pipeline
  * group): select_ms = total ms of the rounds that select (each also backs up
  * the previous batch, thread by thread), backup_ms = total ms of the final

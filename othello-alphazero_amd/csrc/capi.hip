@@ -22,13 +22,17 @@ using namespace oamd;
 
 constexpr int kMaxPipeline = 8;
 constexpr int kEvPerBlock = 4;  // timing events per (round, group): tree begin/end, NN begin/end
-// NN launches of the pipeline groups run one after another, so each owns every
-// CU while the other groups' tree kernels run beside it and its HIP-event
-// duration is its own. OAMD_NN_ORDER 1: a token event passed between the group
-// streams; 2: all NN launches on one NN stream (a group's launch waits for its
-// select, its backup for the launch); 0: unordered (A/B only). Kernel traces
-// show the same gap between consecutive launches for 1 and 2 (~14 us, ~24 us
-// with the timing events), and 1 measured 0.4 % faster in the bench.
+// Order of the pipeline groups' NN launches within an NN chain (one chain:
+// one after another, each owning every CU while the other groups' tree
+// kernels run beside it). OAMD_NN_ORDER 1: a token event passed between the
+// group streams; 2: all NN launches on one NN stream (a group's launch waits
+// for its select, its backup for the launch); 0: unordered (A/B only). Kernel
+// traces show the same gap between consecutive launches for 1 and 2 (~14 us,
+// ~24 us with the timing events), and 1 measured 0.4 % faster in the bench.
+// The default is one chain per group (2 groups, 2 chains): a group's launch
+// starts as soon as its selection is done, so it fills the other launch's
+// last-generation tail and the launch gap (bench +2.5-2.8 %, two boxes;
+// DESIGN.md §7).
 #ifndef OAMD_NN_ORDER
 #define OAMD_NN_ORDER 1
 #endif
@@ -178,7 +182,7 @@ struct oamd_engine {
     // another, chains run concurrently (1 = every launch serialised)
     static constexpr int kMaxChains = 4;
     hipEvent_t nn_token[kMaxChains] = {};
-    int nn_chains = 1;
+    int nn_chains = 2;
     hipStream_t nn_stream = nullptr;
     hipEvent_t sel_ev[kMaxPipeline] = {};
     hipEvent_t nn_ev[kMaxPipeline] = {};
@@ -198,6 +202,7 @@ struct oamd_engine {
     int64_t ev_rows[2] = {0, 0};
     int ev_cur = 0;
     float nn_ms = 0.0f;
+    float nn_busy_ms = 0.0f;  // union of the timed NN launch intervals
     float select_ms = 0.0f;
     float backup_ms = 0.0f;
     int64_t nn_launches = 0;
@@ -207,6 +212,10 @@ struct oamd_engine {
     int resolve_timing(int p) {
         const int n = ev_blocks[p];
         if (!n) return OAMD_OK;
+        // NN launch intervals relative to the search's first event: their
+        // union is the time some ResNet launch ran (launches of different NN
+        // chains overlap; with one chain the union is the sum of durations)
+        std::vector<std::pair<float, float>> iv;
         for (int i = 0; i < n; ++i) {
             const hipEvent_t* b = &ev[p][kEvPerBlock * i];
             float ms = 0.0f;
@@ -220,8 +229,24 @@ struct oamd_engine {
             if (nn) {
                 HIPCHK(hipEventElapsedTime(&ms, b[2], b[3]));
                 nn_ms += ms;
+                float t0 = 0.0f, t1 = 0.0f;
+                HIPCHK(hipEventElapsedTime(&t0, ev[p][0], b[2]));
+                HIPCHK(hipEventElapsedTime(&t1, ev[p][0], b[3]));
+                iv.emplace_back(t0, t1);
             }
         }
+        std::sort(iv.begin(), iv.end());
+        float lo = 0.0f, hi = -1.0f;
+        for (const auto& x : iv) {
+            if (x.first > hi) {
+                if (hi > lo) nn_busy_ms += hi - lo;
+                lo = x.first;
+                hi = x.second;
+            } else if (x.second > hi) {
+                hi = x.second;
+            }
+        }
+        if (hi > lo) nn_busy_ms += hi - lo;
         nn_launches += ev_launches[p];
         tree_launches += ev_final[p];
         nn_rows += ev_rows[p];
@@ -866,6 +891,13 @@ int oamd_engine_nn_timing(const oamd_engine* ce, float* nn_ms, int64_t* launches
     if (nn_ms) *nn_ms = e->nn_ms;
     if (launches) *launches = e->nn_launches;
     if (rows) *rows = e->nn_rows;
+    return OAMD_OK;
+}
+
+int oamd_engine_nn_busy(const oamd_engine* ce, float* busy_ms) {
+    oamd_engine* e = const_cast<oamd_engine*>(ce);
+    if (int rc = e->resolve_all_timing()) return rc;
+    if (busy_ms) *busy_ms = e->nn_busy_ms;
     return OAMD_OK;
 }
 

@@ -674,6 +674,11 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
             check(oamd_engine_nn_timing(e.h, &ms, &launches, &rows));
             return py::make_tuple(ms, launches, rows);
         })
+        .def("nn_busy", [](Engine& e) {
+            float ms = 0.0f;
+            check(oamd_engine_nn_busy(e.h, &ms));
+            return ms;
+        })
         .def("work_counters", [](Engine& e) {
             int64_t sims = 0, evals = 0;
             check(oamd_engine_work_counters(e.h, &sims, &evals));

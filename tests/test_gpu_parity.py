@@ -10,7 +10,6 @@ Bars (DESIGN.md "Parity"):
 """
 
 import json
-import os
 
 import numpy as np
 import pytest
@@ -446,11 +445,14 @@ def test_gpu_async_search_matches_sync(om):
         sel, bk, launches2 = b.engine.tree_timing()
         steps = 64 // 32
         assert launches2 == moves * steps * 2  # 2 pipeline groups at G >= 64
-        # prioritised groups (opt-in OAMD_NN_PRIO=1): only group 0's NN launches carry events
-        timed_groups = 1 if os.environ.get("OAMD_NN_PRIO", "0") not in ("", "0") else 2
+        timed_groups = 2  # every group's NN launches carry events
         assert launches == moves * steps * timed_groups
         assert rows == moves * steps * (G // 2) * 32 * timed_groups
         assert ms > 0 and sel > 0 and bk > 0
+        # union of the launch intervals: at most their summed durations (two NN
+        # chains by default, so the groups' launches may overlap)
+        busy = b.engine.nn_busy()
+        assert 0 < busy <= ms * 1.0001
         return torch.stack(acts).cpu().numpy(), [b.visit_counts(g) for g in range(G)]
 
     a_sync, v_sync = play(True)

@@ -175,6 +175,37 @@ def trace_summary(outdir: str, name: str, tag: str) -> None:
     stats = next(Path(outdir).glob(f"trace_{name}/**/run_kernel_stats.csv"))
     OUT.mkdir(exist_ok=True)
     shutil.copy(stats, OUT / f"{tag}_kernel_stats.csv")
+    trace = next(Path(outdir).glob(f"trace_{name}/**/run_kernel_trace.csv"), None)
+    if trace is not None:
+        res = resnet_busy(trace)
+        (OUT / f"{tag}_resnet_busy.json").write_text(json.dumps(res, indent=1) + "\n")
+        print(json.dumps(res, indent=1))
+
+
+def resnet_busy(trace: Path) -> dict:
+    """k_resnet dispatches of a kernel trace: mean duration, and the union of
+    their [start, end] intervals per dispatch (launches of different NN chains
+    overlap; bench.py's busy_ms_per_launch is the same union from HIP events)."""
+    iv = []
+    with open(trace) as f:
+        for row in csv.DictReader(f):
+            if "k_resnet" in row["Kernel_Name"]:
+                iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+    iv.sort()
+    busy, lo, hi = 0, None, None
+    for a, b in iv:
+        if hi is None or a > hi:
+            if hi is not None:
+                busy += hi - lo
+            lo, hi = a, b
+        else:
+            hi = max(hi, b)
+    if hi is not None:
+        busy += hi - lo
+    n = max(1, len(iv))
+    return {"source": str(trace), "dispatches": len(iv),
+            "avg_duration_ms": round(sum(b - a for a, b in iv) / n / 1e6, 4),
+            "busy_ms_per_dispatch": round(busy / n / 1e6, 4)}
 
 
 if __name__ == "__main__":
