@@ -274,6 +274,10 @@ def parse_args(argv: list[str]):
     ap.add_argument("--round-robin-endgames", action="store_true",
                     help="all-terminal batches wait for their round instead of the reference's immediate "
                          "re-selection (oamd_engine_set_exact_interleaving(0)); default: exact")
+    ap.add_argument("--chain-budget", type=int, default=8,
+                    help="re-selections after all-terminal batches per game and round before the chain is split "
+                         "(0 = never split; exact interleaving only)")
+    ap.add_argument("--chain-cuts", type=int, default=3, help="chain splits per game and search (= extra rounds)")
     ap.add_argument("--cpu-baseline-moves", type=int, default=24,
                     help="timed moves of the CPU baseline (0 = skip it), after 2 warm-up moves")
     ap.add_argument("--cpu-baseline-threads", type=int, default=0,
@@ -363,6 +367,7 @@ class EngineWorkload:
             self.b.engine.set_pipeline(args.pipeline)
         self.b.engine.set_nn_chains(args.nn_chains)
         self.b.engine.set_exact_interleaving(not args.round_robin_endgames)
+        self.b.engine.set_chain_split(args.chain_budget, args.chain_cuts)
         props = torch.cuda.get_device_properties(local)
         self.device_id = f"{os.uname().nodename}:{getattr(props, 'uuid', local)}"
 
@@ -461,7 +466,9 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
                                if n_devices < world else "")),
             "ranks": ranks,
             "backend": (backend if world > 1 else "none"),
-            "endgame_interleaving": "round-robin" if args.round_robin_endgames else "exact (reference)",
+            "endgame_interleaving": ("round-robin" if args.round_robin_endgames else
+                                     f"exact (reference), chains split after {args.chain_budget} re-selections, "
+                                     f"<= {args.chain_cuts} times per search"),
             "calls": ("search + selfplay_move per step" if args.per_move_calls or args.sync_search
                       else f"one selfplay_steps call for the {args.steps} timed steps"),
         },

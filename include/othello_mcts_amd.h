@@ -177,6 +177,16 @@ int oamd_engine_set_nn_batch(oamd_engine *e, int32_t rows);
  * chains run concurrently (the default lets the two groups' launches overlap
  * at their ends). Results do not depend on it. */
 int oamd_engine_set_nn_chains(oamd_engine *e, int32_t chains);
+/* Native search with the exact interleaving: a virtual thread whose batches
+ * come back all terminal selects again at once (search_thread.cpp:102-127),
+ * which near a game's end can run a thread's whole remaining search inside one
+ * round and hold its pipeline group's ResNet launch. After `budget`
+ * re-selections in a round such a chain stops and the game's next round
+ * resumes it exactly there (every game keeps its order of operations; only
+ * round boundaries move), at most `cuts` times per search, at the cost of
+ * `cuts` extra rounds per search. Default budget 8, cuts 3; budget 0 = never
+ * split. Results do not depend on it. */
+int oamd_engine_set_chain_split(oamd_engine *e, int32_t budget, int32_t cuts);
 /* enable = 1 (default): the reference's thread interleaving exactly — a
  * virtual thread whose batch is all terminal backs it up without an NN round
  * trip and selects again at once (search_thread.cpp:102-127), in the same

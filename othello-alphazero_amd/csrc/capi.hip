@@ -167,6 +167,11 @@ struct oamd_engine {
     int steps_left = 0;
     int steps_total = 0;  // of the step-wise search begun by oamd_engine_search_begin
     bool exact_interleaving = true;  // oamd_engine_set_exact_interleaving
+    // native search, exact interleaving: an all-terminal chain stops after
+    // chain_budget re-selections in a round, at most chain_cuts times per
+    // search (k_tree); chain_cuts extra rounds per search. 0 = never split
+    int chain_budget = 8;
+    int chain_cuts = 3;
     int step_phase = 0;  // 1 = a selected round awaits its backup (step API)
     // pipeline groups (0 = auto) and their streams / fork-join events
     int pipeline = 0;
@@ -989,22 +994,30 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
     const int T = e->cfg.num_threads, B = e->cfg.batch_size;
     const int pool = e->ev_cur;
     const int nch = e->nn_chains < K ? e->nn_chains : K;
-    // rounds 0..steps (k_tree): round s backs up batch s-1 and selects batch s,
-    // thread by thread; the NN evaluates batch s between rounds s and s+1
-    for (int s = 0; s <= steps; ++s) {
+    // chain splitting (k_tree): X extra rounds absorb the rounds a split chain
+    // delays its game by; only the reference's interleaving has chains
+    const int X = e->exact_interleaving && e->chain_budget > 0 ? e->chain_cuts : 0;
+    const int budget = X > 0 ? e->chain_budget : 0;
+    const int S = steps + X;
+    // rounds 0..S (k_tree): round s backs up what the previous rounds selected
+    // and selects, thread by thread; the NN evaluates round s's selections
+    // between rounds s and s+1; the last round only backs up. Timing events:
+    // rounds 0..steps-1 and the last one (the extra rounds are not timed)
+    for (int s = 0; s <= S; ++s) {
+        const int blk = s < steps ? s : (s == S ? steps : -1);
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)P.g0[k] * L;
             hipStream_t sk = P.st[k];
-            hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
+            hipEvent_t* ev = timed && blk >= 0 ? &e->ev[pool][kEvPerBlock * (blk * K + k)] : nullptr;
             if (ev) HIPCHK(hipEventRecord(ev[0], sk));
             // evaluation list of group k: round s fills counter s % 2 and zeroes
             // the other one (which round s-1's launch, done by now, read); the
             // final round zeroes counter 0 for the next search's round 0
             int* cnt = e->rowcount + 2 * k;
-            launch_tree(E, sk, s > 0, s < steps, T, B, P.g0[k], P.ng[k], 0, -1, s < steps ? cnt + (s & 1) : nullptr,
-                        s < steps ? cnt + ((s + 1) & 1) : cnt, s == 0);
+            launch_tree(E, sk, s > 0, s < S, T, B, P.g0[k], P.ng[k], 0, -1, s < S ? cnt + (s & 1) : nullptr,
+                        s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X);
             if (ev) HIPCHK(hipEventRecord(ev[1], sk));
-            if (s == steps) continue;
+            if (s == S) continue;
             // the groups' NN launches run one after another (OAMD_NN_ORDER)
             hipStream_t ns = sk;
             if (K > 1 && OAMD_NN_ORDER == 2) {
@@ -1144,6 +1157,13 @@ int oamd_engine_set_nn_chains(oamd_engine* e, int32_t chains) {
     if (chains < 1 || chains > oamd_engine::kMaxChains)
         return fail(OAMD_INVALID_ARGUMENT, "nn chains must be in [1, " + std::to_string(oamd_engine::kMaxChains) + "]");
     e->nn_chains = chains;
+    return OAMD_OK;
+}
+
+int oamd_engine_set_chain_split(oamd_engine* e, int32_t budget, int32_t cuts) {
+    if (budget < 0 || cuts < 0 || cuts > 64) return fail(OAMD_INVALID_ARGUMENT, "chain split: budget >= 0, cuts in [0, 64]");
+    e->chain_budget = budget;
+    e->chain_cuts = cuts;
     return OAMD_OK;
 }
 

@@ -45,7 +45,9 @@ struct GameState {
     uint64_t event;  // next random event
     int32_t hist[16];  // strict ancestors of the root: parent, grandparent, ...
     int32_t ply;       // moves played since the last reset (self-play driver)
-    int32_t pad[3];
+    int32_t resume;    // k_tree chain splitting: the virtual thread this game's next round starts at
+    int32_t cuts;      // ... and the chains split so far in this search
+    int32_t pad[1];
 };
 
 // Packed NN input row (FW uint64 words): word 0 = meta, then (p1, p2) of the

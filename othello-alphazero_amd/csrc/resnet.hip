@@ -692,6 +692,9 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     if (M.list) {  // entries filled this round (a uniform scalar load)
         const int filled = *M.count - M.off;
         M.rows = filled < M.rows ? (filled > 0 ? filled : 0) : M.rows;
+        // a workgroup past the filled entries has nothing to do: it leaves
+        // before its first weight DMA (the launch's grid is the list capacity)
+        if (row0 >= M.rows) return;
     }
     OAMD_STAMP(0);
 #ifdef OAMD_STAMPS

@@ -477,8 +477,19 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
 // non-terminal leaves this round selects are appended to E.rowlist[g0 * L ..]
 // behind the counter *cnt_add; *cnt_reset (the counter of the next round,
 // which no launch still reads) is zeroed by the group's first wave.
+// Chain splitting (budget > 0, the native search): a thread whose batches
+// come back all terminal selects again at once (the reference's order), and
+// such a chain can run to the end of the thread's search inside one round,
+// holding its pipeline group's NN launch. After `budget` re-selections in a
+// round the game stops (at most `max_cuts` times per search) and its next
+// round resumes exactly there, visiting the threads cyclically from that
+// thread: every game still performs the same operations in the same order,
+// only the round boundaries move. Each cut delays the game's remaining visits
+// by at most one round, so the host runs max_cuts extra rounds. budget = 0:
+// rounds always start at thread 0 (the step API and the single-game split).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree(EngineView E, int g0, int do_backup, int do_select,
-                                             int t0, int t1, int B, int* cnt_add, int* cnt_reset, int fresh) {
+                                             int t0, int t1, int B, int* cnt_add, int* cnt_reset, int fresh,
+                                             int budget, int max_cuts) {
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
@@ -505,7 +516,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     unsigned long long sims = 0, evals = 0;
     int count = gs->count;
     bool overflow = false;
-    for (int t = t0; t < t1; ++t) {
+    const int nt = t1 - t0;
+    const int rp = budget > 0 && !fresh ? gs->resume : t0;  // this round's first thread
+    int cuts = budget > 0 && !fresh ? gs->cuts : 0;
+    int chain = 0;     // re-selections after all-terminal batches in this round
+    int cut_at = -1;   // the thread whose chain this round stopped
+    // a search's first round starts every thread fresh, also the ones a split
+    // chain keeps it from visiting (their state is read from the next round on)
+    if (fresh && budget > 0 && lane < nt) E.tstate[(size_t)g * E.L + t0 + lane] = 0;
+    for (int k = 0; k < nt && cut_at < 0; ++k) {
+        const int t = t0 + (rp - t0 + k) % nt;
         // virtual thread t: batches selected so far in this search, and whether
         // its last batch waits for the NN (a search's first round starts fresh)
         int* ts = E.tstate + (size_t)g * E.L + t;
@@ -519,17 +539,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
         // the thread's next batch; one whose leaves are all terminal needs no NN
         // round trip (search_thread.cpp:102) and is backed up at once (:116-127),
         // then the thread selects again, up to `steps` batches per search
+        bool again = false;  // the last batch was all terminal and is backed up
         while (do_select && !pend && sel < E.steps) {
+            if (again && budget > 0 && chain >= budget && cuts < max_cuts) {
+                cut_at = t;  // the next round continues this chain
+                ++cuts;
+                break;
+            }
             const unsigned long long ev0 = evals;
             select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals, cnt_add,
                          g0 * E.L);
             ++sel;
-            if (evals != ev0 || !E.terminal_skip) pend = true;
-            else backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
+            if (evals != ev0 || !E.terminal_skip) {
+                pend = true;
+            } else {
+                backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
+                again = true;
+                ++chain;
+            }
         }
         if (lane == 0) *ts = sel | (pend ? 1 << 16 : 0);
     }
     if (lane == 0) {
+        if (budget > 0) {
+            gs->resume = cut_at >= 0 ? cut_at : rp;
+            gs->cuts = cuts;
+        }
         gs->event = event;
         gs->count = count;
         // atomic like select_range's kDepthCap: a plain read-modify-write of
@@ -942,13 +977,14 @@ __global__ void k_apply_positions(const Pos* in, const int32_t* actions, Pos* ou
 static inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
-                 int g0, int ng, int t0, int t1, int* cnt_add, int* cnt_reset, bool fresh) {
+                 int g0, int ng, int t0, int t1, int* cnt_add, int* cnt_reset, bool fresh, int budget,
+                 int max_cuts) {
     if (ng < 0) ng = E.G - g0;
     if (t1 < 0) t1 = T;
     if (T * B != E.L || t0 < 0 || t1 > T || t0 >= t1) return;  // caller validated; never launch on a mismatched layout
     if (ng > 0 && (do_backup || do_select))
         hipLaunchKernelGGL(k_tree, dim3(ng), dim3(64), 0, s, E, g0, (int)do_backup, (int)do_select, t0, t1, B,
-                           do_select ? cnt_add : nullptr, cnt_reset, (int)fresh);
+                           do_select ? cnt_add : nullptr, cnt_reset, (int)fresh, budget, max_cuts);
 }
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s) {
     if (rows > 0) hipLaunchKernelGGL(k_features_f32, dim3(blocks_for(rows, 4)), dim3(256), 0, s, E, out, row_begin, rows);

@@ -272,3 +272,41 @@ def test_selfplay_steps_equal_move_by_move(om, G, pipeline):
         assert restarts > 0
     numerics.record(f"selfplay_steps G={G} pipeline={pipeline or 'auto'}",
                     f"{n} moves identical to search + selfplay_move, {restarts} game ends")
+
+
+def test_chain_split_keeps_every_game_identical(om):
+    """Chain splitting (oamd_engine_set_chain_split): near a game's end a thread
+    whose batches come back all terminal re-selects at once (the reference's
+    order) and the native search may stop such a chain and resume it in the
+    game's next round. Games late in their play, 10 batches per thread and
+    search: budgets 1 and 4 (and no splitting) give the callback path's visits,
+    Q, moves and finish codes move after move."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(43, 9, 128, 1, 32), device=0)
+    kw = dict(history_size=4, num_simulations=320, num_threads=2, batch_size=16, dirichlet_epsilon=0.25, seed=8,
+              node_capacity=1 << 17)
+    splits = [(0, 0), (1, 3), (4, 4)]
+    engines = [om.BatchedMCTS(64, **kw) for _ in splits]
+    for x, (budget, cuts) in zip(engines, splits):
+        x.engine.set_chain_split(budget, cuts)
+    ref = om.BatchedMCTS(64, **kw)
+    for x in engines + [ref]:
+        x.random_openings(50, seed=9)
+    total_sims = total_evals = 0
+    for mv in range(24):
+        sr, er = ref.search(lambda f: net(f))
+        total_sims += sr
+        total_evals += er
+        vr, qr = ref.root_stats()
+        xr = ref.selfplay_move(temperature_moves=12, opening_moves=50)
+        for x, sp in zip(engines, splits):
+            assert x.search(net) == (sr, er), (mv, sp)
+            v, q = x.root_stats()
+            assert torch.equal(v, vr) and torch.equal(q, qr), (mv, sp)
+            o = x.selfplay_move(temperature_moves=12, opening_moves=50)
+            assert torch.equal(o["actions"], xr["actions"]) and torch.equal(o["finished"], xr["finished"]), (mv, sp)
+    share = 1.0 - total_evals / total_sims
+    numerics.record("chain split", f"64 late games x 24 moves: terminal-leaf share {share:.3f}, "
+                                   "budgets 0/1/4 == callback")
+    assert share > 0.1
