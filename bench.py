@@ -397,13 +397,14 @@ class EngineWorkload:
 
     def stop_measuring(self) -> dict:
         e = self.b.engine
-        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), bu0 = self.t0
-        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), bu1 = e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy()
+        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), (bu0, ts0, te0) = self.t0
+        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), (bu1, ts1, te1) = (e.nn_timing(), e.tree_timing(),
+                                                                         e.work_counters(), e.nn_busy())
         overflow_games, depth_capped = e.status()
         if overflow_games or depth_capped:
             raise SystemExit(f"bench invalid: {overflow_games} game(s) overflowed their node pool, "
                              f"{depth_capped} hit the depth cap")
-        return {"nn_ms": ms1 - ms0, "nn_busy_ms": bu1 - bu0, "nn_launches": la1 - la0, "nn_rows": rw1 - rw0, "select_ms": se1 - se0,
+        return {"nn_ms": ms1 - ms0, "nn_busy_ms": bu1 - bu0, "timed_evals": te1 - te0, "nn_launches": la1 - la0, "nn_rows": rw1 - rw0, "select_ms": se1 - se0,
                 "backup_ms": bk1 - bk0, "tree_launches": tl1 - tl0, "sims": si1 - si0, "evals": ev1 - ev0,
                 "overflow_games": overflow_games}
 
@@ -504,9 +505,12 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     rows_launched = args.games * args.threads * args.batch * ((args.sims + args.threads * args.batch - 1)
                                                               // (args.threads * args.batch)) * args.steps
     eval_share = m["evals"] / max(1, rows_launched)
-    n_eval_per_launch = rows_per_launch * eval_share
+    # the timed searches' own NN rows (device counters of exactly those
+    # searches: their extra chain-splitting rounds' small launches included)
+    n_eval_per_launch = m["timed_evals"] / max(1, m["nn_launches"])
     achieved = flops * n_eval_per_launch / (busy_ms * 1e-3) / 1e12
-    achieved_launched = flops * rows_per_launch / (busy_ms * 1e-3) / 1e12
+    # every launched row counted as work (the round-2 basis): n_eval / eval_share
+    achieved_launched = achieved / max(eval_share, 1e-9)
     executed = flops - 2.0 * 64 * 9 * args.channels * args.channels * 2 * R // 12
     peak = PEAK_TFLOPS[args.dtype]
     # HBM bytes per launch from the committed PMC summary of this same workload
@@ -532,8 +536,11 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     # back up the previous batch and select the next, the final round backs up
     tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch)}
     steps_per_search = (args.sims + args.threads * args.batch - 1) // (args.threads * args.batch)
+    # selecting rounds per search: the batches per thread + the chain-splitting extra rounds
+    rounds = steps_per_search + (args.chain_cuts if args.chain_budget > 0 and not args.round_robin_endgames else 0)
+    tree["rounds_per_search"] = rounds + 1
     for name, ms, n in (("k_tree", m["select_ms"], m["tree_launches"]),
-                        ("k_tree_final_backup", m["backup_ms"], m["tree_launches"] // steps_per_search)):
+                        ("k_tree_final_backup", m["backup_ms"], m["tree_launches"] // rounds)):
         avg = ms / max(1, n)
         entry = {"avg_launch_ms": round(avg, 4)}
         if name in tree_bytes:
@@ -553,9 +560,9 @@ def measured_fields(args, m: dict, workload: str) -> dict:
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
-            "basis": ("n_eval rows (non-terminal leaves) per launch x flops_per_row / busy ms per launch "
-                      "(the union of the timed launch intervals / launches; = avg_launch_ms when launches do "
-                      "not overlap)"),
+            "basis": ("n_eval rows (the timed searches' non-terminal leaves) per launch x flops_per_row / busy "
+                      "ms per launch (the union of the timed launch intervals / launches; = avg_launch_ms when "
+                      "launches do not overlap)"),
             "avg_launch_ms": round(avg_ms, 4),
             "busy_ms_per_launch": round(busy_ms, 4),
             "nn_chains": args.nn_chains,

@@ -304,8 +304,10 @@ int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches,
 /* The union of those NN launch intervals (ms some timed ResNet launch was
  * running): equal to nn_ms when launches never overlap (one NN chain); with
  * oamd_engine_set_nn_chains(e, n > 1) the groups' launches overlap and nn_ms
- * counts the shared time once per launch. */
-int oamd_engine_nn_busy(const oamd_engine *e, float *busy_ms);
+ * counts the shared time once per launch. timed_sims / timed_evals: the
+ * simulations and NN rows (non-terminal leaves) of those same timed searches,
+ * so evals x FLOPs per row / busy is the delivered rate. */
+int oamd_engine_nn_busy(const oamd_engine *e, float *busy_ms, int64_t *timed_sims, int64_t *timed_evals);
 /* Same for the tree kernel (k_tree, one launch per search round and pipeline
  * group): select_ms = total ms of the rounds that select (each also backs up
  * the previous batch, thread by thread), backup_ms = total ms of the final

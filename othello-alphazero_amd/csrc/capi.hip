@@ -754,7 +754,7 @@ int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity,
     e->seed = seed;
     const size_t nodes = (size_t)num_games * node_capacity;
     if ((rc = dalloc(&e->link, nodes)) || (rc = dalloc(&e->stat, nodes)) || (rc = dalloc(&e->pos, nodes)) ||
-        (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) || (rc = dalloc(&e->counters, 4)) ||
+        (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) || (rc = dalloc(&e->counters, 6)) ||
         (rc = dalloc(&e->rowcount, 2 * kMaxPipeline)) ||
         (rc = dalloc(&e->status_dev, 2)) || (rc = dalloc(&e->info_dev, num_games)) || (rc = dalloc(&e->visits_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->q_dev, (size_t)num_games * 65)) ||
@@ -763,7 +763,7 @@ int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity,
         delete e;
         return rc;
     }
-    if (hipMemset(e->counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMemset(e->counters, 0, 6 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(e->rowcount, 0, 2 * kMaxPipeline * sizeof(int32_t)) != hipSuccess) {
         delete e;
         return fail(OAMD_RUNTIME, "engine init: counter memset failed");
@@ -899,10 +899,17 @@ int oamd_engine_nn_timing(const oamd_engine* ce, float* nn_ms, int64_t* launches
     return OAMD_OK;
 }
 
-int oamd_engine_nn_busy(const oamd_engine* ce, float* busy_ms) {
+int oamd_engine_nn_busy(const oamd_engine* ce, float* busy_ms, int64_t* timed_sims, int64_t* timed_evals) {
     oamd_engine* e = const_cast<oamd_engine*>(ce);
     if (int rc = e->resolve_all_timing()) return rc;
     if (busy_ms) *busy_ms = e->nn_busy_ms;
+    if (timed_sims || timed_evals) {
+        DeviceGuard dg(e->device);
+        unsigned long long c[2] = {0, 0};
+        HIPCHK(hipMemcpy(c, e->counters + 4, sizeof(c), hipMemcpyDeviceToHost));
+        if (timed_sims) *timed_sims = (int64_t)c[0];
+        if (timed_evals) *timed_evals = (int64_t)c[1];
+    }
     return OAMD_OK;
 }
 
@@ -987,6 +994,12 @@ static void timing_end(oamd_engine* e, int steps, int NB, bool split, const Grou
 // streams (already forked from the engine stream). chained: the groups'
 // streams carry on from a previous search of the same call (a multi-move
 // self-play call), so its first NN launch also waits for the NN token.
+// Extra rounds of a native grouped search (chain splitting, k_tree): the
+// reference's interleaving only
+static int extra_rounds(const oamd_engine* e) {
+    return e->exact_interleaving && e->chain_budget > 0 ? e->chain_cuts : 0;
+}
+
 static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPlan& P, int steps, bool timed,
                                 bool chained) {
     const EngineView E = e->view();
@@ -996,26 +1009,25 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
     const int nch = e->nn_chains < K ? e->nn_chains : K;
     // chain splitting (k_tree): X extra rounds absorb the rounds a split chain
     // delays its game by; only the reference's interleaving has chains
-    const int X = e->exact_interleaving && e->chain_budget > 0 ? e->chain_cuts : 0;
+    const int X = extra_rounds(e);
     const int budget = X > 0 ? e->chain_budget : 0;
     const int S = steps + X;
     // rounds 0..S (k_tree): round s backs up what the previous rounds selected
     // and selects, thread by thread; the NN evaluates round s's selections
-    // between rounds s and s+1; the last round only backs up. Timing events:
-    // rounds 0..steps-1 and the last one (the extra rounds are not timed)
+    // between rounds s and s+1; the last round only backs up. A timed search
+    // records events for every round and counts its work (counters [4..5])
     for (int s = 0; s <= S; ++s) {
-        const int blk = s < steps ? s : (s == S ? steps : -1);
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)P.g0[k] * L;
             hipStream_t sk = P.st[k];
-            hipEvent_t* ev = timed && blk >= 0 ? &e->ev[pool][kEvPerBlock * (blk * K + k)] : nullptr;
+            hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
             if (ev) HIPCHK(hipEventRecord(ev[0], sk));
             // evaluation list of group k: round s fills counter s % 2 and zeroes
             // the other one (which round s-1's launch, done by now, read); the
             // final round zeroes counter 0 for the next search's round 0
             int* cnt = e->rowcount + 2 * k;
             launch_tree(E, sk, s > 0, s < S, T, B, P.g0[k], P.ng[k], 0, -1, s < S ? cnt + (s & 1) : nullptr,
-                        s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X);
+                        s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X, timed);
             if (ev) HIPCHK(hipEventRecord(ev[1], sk));
             if (s == S) continue;
             // the groups' NN launches run one after another (OAMD_NN_ORDER)
@@ -1089,14 +1101,15 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     // sampled timing: per (round, group) kEvPerBlock events: tree begin/end, NN
     // begin/end (on the NN stream, after its waits; not in the final round)
     bool timed = false;
-    if ((rc = timing_begin(e, steps, NB, &timed))) return rc;
+    const int S = split ? steps : steps + extra_rounds(e);  // rounds that select
+    if ((rc = timing_begin(e, S, NB, &timed))) return rc;
     const int pool = e->ev_cur;
     for (int s = 0; split && s <= steps; ++s) {
         for (int t = 0; t < T; ++t) {
             hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * T + t)] : nullptr;
             if (s > 0) HIPCHK(hipStreamWaitEvent(e->stream, e->nn_ev[t], 0));  // thread t's batch s-1 evaluated
             if (ev) HIPCHK(hipEventRecord(ev[0], e->stream));
-            launch_tree(E, e->stream, s > 0, s < steps, T, B, 0, 1, t, t + 1, nullptr, nullptr, s == 0);
+            launch_tree(E, e->stream, s > 0, s < steps, T, B, 0, 1, t, t + 1, nullptr, nullptr, s == 0, 0, 0, timed);
             if (ev) HIPCHK(hipEventRecord(ev[1], e->stream));
             if (s == steps) continue;
             hipStream_t ns = e->pipe_stream[t % 2];
@@ -1115,7 +1128,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     }
     LAUNCHCHK();
     if (!split && (rc = join_groups(e, P))) return rc;
-    if (timed) timing_end(e, steps, NB, split, P);
+    if (timed) timing_end(e, S, NB, split, P);
     // without counters requested the search is left in flight (stream order)
     if (sims || evals) {
         unsigned long long c[2] = {0, 0};
@@ -1318,12 +1331,12 @@ int oamd_engine_selfplay_steps(oamd_engine* e, oamd_net* net, const oamd_selfpla
     int rc = fork_groups(e, P);
     for (int i = 0; !rc && i < n_moves; ++i) {
         bool timed = false;
-        if ((rc = timing_begin(e, steps, P.K, &timed))) break;
+        if ((rc = timing_begin(e, steps + extra_rounds(e), P.K, &timed))) break;
         if ((rc = enqueue_group_rounds(e, N, P, steps, timed, i > 0))) break;
         for (int k = 0; k < P.K; ++k)
             launch_selfplay_move(E, sp, P.g0[k], P.ng[k], out(i, actions_dev, 1), out(i, finished_dev, 1),
                                  out(i, features_dev, 8 * C * 64), out(i, policy_dev, 8 * 65), P.st[k]);
-        if (timed) timing_end(e, steps, P.K, false, P);
+        if (timed) timing_end(e, steps + extra_rounds(e), P.K, false, P);
     }
     if (rc) return rc;
     LAUNCHCHK();

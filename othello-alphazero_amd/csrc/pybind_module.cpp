@@ -678,8 +678,9 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
         })
         .def("nn_busy", [](Engine& e) {
             float ms = 0.0f;
-            check(oamd_engine_nn_busy(e.h, &ms));
-            return ms;
+            int64_t sims = 0, evals = 0;
+            check(oamd_engine_nn_busy(e.h, &ms, &sims, &evals));
+            return py::make_tuple(ms, sims, evals);
         })
         .def("work_counters", [](Engine& e) {
             int64_t sims = 0, evals = 0;

@@ -436,6 +436,7 @@ def test_gpu_async_search_matches_sync(om):
                            node_capacity=1 << 17)
         b.random_openings(6, seed=4)
         b.engine.enable_timing(True)
+        b.engine.set_chain_split(8, 3)  # 3 extra rounds per search (chain splitting)
         acts = []
         for _ in range(moves):
             r = b.search(net, sync=sync)
@@ -443,7 +444,7 @@ def test_gpu_async_search_matches_sync(om):
             acts.append(b.selfplay_move(temperature_moves=3, emit_targets=False)["actions"].clone())
         ms, launches, rows = b.engine.nn_timing()
         sel, bk, launches2 = b.engine.tree_timing()
-        steps = 64 // 32
+        steps = 64 // 32 + 3
         assert launches2 == moves * steps * 2  # 2 pipeline groups at G >= 64
         timed_groups = 2  # every group's NN launches carry events
         assert launches == moves * steps * timed_groups
@@ -451,8 +452,9 @@ def test_gpu_async_search_matches_sync(om):
         assert ms > 0 and sel > 0 and bk > 0
         # union of the launch intervals: at most their summed durations (two NN
         # chains by default, so the groups' launches may overlap)
-        busy = b.engine.nn_busy()
+        busy, tsims, tevals = b.engine.nn_busy()
         assert 0 < busy <= ms * 1.0001
+        assert tsims == moves * G * 64 and 0 < tevals <= tsims  # every search timed (stride 1)
         return torch.stack(acts).cpu().numpy(), [b.visit_counts(g) for g in range(G)]
 
     a_sync, v_sync = play(True)
