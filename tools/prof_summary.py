@@ -153,7 +153,9 @@ def bench_summary(outdir: str, prefix: str, tag: str) -> dict:
             for ln in log.read_text().splitlines():
                 if ln.startswith("{") and '"metric"' in ln:
                     bench = json.loads(ln)
-    rows = bench["roofline"]["rows_per_launch"] if bench else None
+    # the NN rows a launch evaluates on average (the bench line's n_eval per
+    # launch: evaluation lists and the small extra chain-splitting rounds)
+    rows = bench["roofline"].get("n_eval_per_launch", bench["roofline"]["rows_per_launch"]) if bench else None
     fpr = bench["roofline"]["flops_per_row"] if bench else None
     res = {"tag": tag, "source": f"tools/gpu.sh pmc {prefix}_* over bench.py",
            "workload": bench["config"]["workload"] if bench else None,
@@ -165,7 +167,7 @@ def bench_summary(outdir: str, prefix: str, tag: str) -> dict:
     if "hbm_bytes_per_launch" in res["derived"] and bench:
         (OUT / "traffic_resnet.json").write_text(json.dumps({
             "tag": tag, "bytes_per_launch": res["derived"]["hbm_bytes_per_launch"],
-            "workload": bench["config"]["workload"], "rows_per_launch": rows,
+            "workload": bench["config"]["workload"], "rows_per_launch": bench["roofline"]["rows_per_launch"],
             "note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> B) per k_resnet launch, rocprofv3 --pmc, separate passes "
                     "(tools/prof_summary.py)"}, indent=1) + "\n")
     return res
