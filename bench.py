@@ -505,8 +505,8 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     rows_launched = args.games * args.threads * args.batch * ((args.sims + args.threads * args.batch - 1)
                                                               // (args.threads * args.batch)) * args.steps
     eval_share = m["evals"] / max(1, rows_launched)
-    # the timed searches' own NN rows (device counters of exactly those
-    # searches: their extra chain-splitting rounds' small launches included)
+    # the timed searches' own NN rows (device counters of exactly the timed
+    # rounds; the chain-splitting extra rounds' small launches are not timed)
     n_eval_per_launch = m["timed_evals"] / max(1, m["nn_launches"])
     achieved = flops * n_eval_per_launch / (busy_ms * 1e-3) / 1e12
     # every launched row counted as work (the round-2 basis): n_eval / eval_share
@@ -536,11 +536,10 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     # back up the previous batch and select the next, the final round backs up
     tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch)}
     steps_per_search = (args.sims + args.threads * args.batch - 1) // (args.threads * args.batch)
-    # selecting rounds per search: the batches per thread + the chain-splitting extra rounds
-    rounds = steps_per_search + (args.chain_cuts if args.chain_budget > 0 and not args.round_robin_endgames else 0)
-    tree["rounds_per_search"] = rounds + 1
+    # timed rounds per search: the batches per thread (the chain-splitting
+    # extra rounds carry no events) + the final backup
     for name, ms, n in (("k_tree", m["select_ms"], m["tree_launches"]),
-                        ("k_tree_final_backup", m["backup_ms"], m["tree_launches"] // rounds)):
+                        ("k_tree_final_backup", m["backup_ms"], m["tree_launches"] // steps_per_search)):
         avg = ms / max(1, n)
         entry = {"avg_launch_ms": round(avg, 4)}
         if name in tree_bytes:

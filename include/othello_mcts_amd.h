@@ -305,8 +305,10 @@ int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches,
  * running): equal to nn_ms when launches never overlap (one NN chain); with
  * oamd_engine_set_nn_chains(e, n > 1) the groups' launches overlap and nn_ms
  * counts the shared time once per launch. timed_sims / timed_evals: the
- * simulations and NN rows (non-terminal leaves) of those same timed searches,
- * so evals x FLOPs per row / busy is the delivered rate. */
+ * simulations and NN rows (non-terminal leaves) of those same timed searches
+ * and rounds, so evals x FLOPs per row / busy is the delivered rate. Timed
+ * are the rounds 1..ceil(S/L) of every timing_stride-th search; the extra
+ * chain-splitting rounds (oamd_engine_set_chain_split) are not. */
 int oamd_engine_nn_busy(const oamd_engine *e, float *busy_ms, int64_t *timed_sims, int64_t *timed_evals);
 /* Same for the tree kernel (k_tree, one launch per search round and pipeline
  * group): select_ms = total ms of the rounds that select (each also backs up

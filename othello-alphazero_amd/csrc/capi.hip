@@ -1015,19 +1015,22 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
     // rounds 0..S (k_tree): round s backs up what the previous rounds selected
     // and selects, thread by thread; the NN evaluates round s's selections
     // between rounds s and s+1; the last round only backs up. A timed search
-    // records events for every round and counts its work (counters [4..5])
+    // records events for rounds 0..steps-1 and the last one, and counts the
+    // work of rounds 0..steps-1 (counters [4..5]): the extra rounds' small
+    // launches (lagging games only) are left out of both
     for (int s = 0; s <= S; ++s) {
+        const int blk = s < steps ? s : (s == S ? steps : -1);
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)P.g0[k] * L;
             hipStream_t sk = P.st[k];
-            hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
+            hipEvent_t* ev = timed && blk >= 0 ? &e->ev[pool][kEvPerBlock * (blk * K + k)] : nullptr;
             if (ev) HIPCHK(hipEventRecord(ev[0], sk));
             // evaluation list of group k: round s fills counter s % 2 and zeroes
             // the other one (which round s-1's launch, done by now, read); the
             // final round zeroes counter 0 for the next search's round 0
             int* cnt = e->rowcount + 2 * k;
             launch_tree(E, sk, s > 0, s < S, T, B, P.g0[k], P.ng[k], 0, -1, s < S ? cnt + (s & 1) : nullptr,
-                        s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X, timed);
+                        s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X, timed && s < steps);
             if (ev) HIPCHK(hipEventRecord(ev[1], sk));
             if (s == S) continue;
             // the groups' NN launches run one after another (OAMD_NN_ORDER)
@@ -1101,8 +1104,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     // sampled timing: per (round, group) kEvPerBlock events: tree begin/end, NN
     // begin/end (on the NN stream, after its waits; not in the final round)
     bool timed = false;
-    const int S = split ? steps : steps + extra_rounds(e);  // rounds that select
-    if ((rc = timing_begin(e, S, NB, &timed))) return rc;
+    if ((rc = timing_begin(e, steps, NB, &timed))) return rc;
     const int pool = e->ev_cur;
     for (int s = 0; split && s <= steps; ++s) {
         for (int t = 0; t < T; ++t) {
@@ -1128,7 +1130,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     }
     LAUNCHCHK();
     if (!split && (rc = join_groups(e, P))) return rc;
-    if (timed) timing_end(e, S, NB, split, P);
+    if (timed) timing_end(e, steps, NB, split, P);
     // without counters requested the search is left in flight (stream order)
     if (sims || evals) {
         unsigned long long c[2] = {0, 0};
@@ -1331,12 +1333,12 @@ int oamd_engine_selfplay_steps(oamd_engine* e, oamd_net* net, const oamd_selfpla
     int rc = fork_groups(e, P);
     for (int i = 0; !rc && i < n_moves; ++i) {
         bool timed = false;
-        if ((rc = timing_begin(e, steps + extra_rounds(e), P.K, &timed))) break;
+        if ((rc = timing_begin(e, steps, P.K, &timed))) break;
         if ((rc = enqueue_group_rounds(e, N, P, steps, timed, i > 0))) break;
         for (int k = 0; k < P.K; ++k)
             launch_selfplay_move(E, sp, P.g0[k], P.ng[k], out(i, actions_dev, 1), out(i, finished_dev, 1),
                                  out(i, features_dev, 8 * C * 64), out(i, policy_dev, 8 * 65), P.st[k]);
-        if (timed) timing_end(e, steps + extra_rounds(e), P.K, false, P);
+        if (timed) timing_end(e, steps, P.K, false, P);
     }
     if (rc) return rc;
     LAUNCHCHK();

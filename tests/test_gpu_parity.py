@@ -444,7 +444,7 @@ def test_gpu_async_search_matches_sync(om):
             acts.append(b.selfplay_move(temperature_moves=3, emit_targets=False)["actions"].clone())
         ms, launches, rows = b.engine.nn_timing()
         sel, bk, launches2 = b.engine.tree_timing()
-        steps = 64 // 32 + 3
+        steps = 64 // 32  # timed rounds (the 3 extra chain-splitting rounds carry no events)
         assert launches2 == moves * steps * 2  # 2 pipeline groups at G >= 64
         timed_groups = 2  # every group's NN launches carry events
         assert launches == moves * steps * timed_groups
@@ -454,7 +454,7 @@ def test_gpu_async_search_matches_sync(om):
         # chains by default, so the groups' launches may overlap)
         busy, tsims, tevals = b.engine.nn_busy()
         assert 0 < busy <= ms * 1.0001
-        assert tsims == moves * G * 64 and 0 < tevals <= tsims  # every search timed (stride 1)
+        assert 0 < tsims <= moves * G * 64 and 0 < tevals <= tsims  # timed rounds of every search
         return torch.stack(acts).cpu().numpy(), [b.visit_counts(g) for g in range(G)]
 
     a_sync, v_sync = play(True)
