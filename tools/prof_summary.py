@@ -201,21 +201,32 @@ def resnet_busy(trace: Path) -> dict:
         for row in csv.DictReader(f):
             if "k_resnet" in row["Kernel_Name"]:
                 iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
-    iv.sort()
-    busy, lo, hi = 0, None, None
-    for a, b in iv:
-        if hi is None or a > hi:
-            if hi is not None:
-                busy += hi - lo
-            lo, hi = a, b
-        else:
-            hi = max(hi, b)
-    if hi is not None:
-        busy += hi - lo
+    def union(xs):
+        xs = sorted(xs)
+        busy, lo, hi = 0, None, None
+        for a, b in xs:
+            if hi is None or a > hi:
+                if hi is not None:
+                    busy += hi - lo
+                lo, hi = a, b
+            else:
+                hi = max(hi, b)
+        return busy + (hi - lo if hi is not None else 0)
+
     n = max(1, len(iv))
-    return {"source": str(trace), "dispatches": len(iv),
-            "avg_duration_ms": round(sum(b - a for a, b in iv) / n / 1e6, 4),
-            "busy_ms_per_dispatch": round(busy / n / 1e6, 4)}
+    res = {"source": str(trace), "dispatches": len(iv),
+           "avg_duration_ms": round(sum(b - a for a, b in iv) / n / 1e6, 4),
+           "busy_ms_per_dispatch": round(union(iv) / n / 1e6, 4)}
+    # without the chain-splitting extra rounds' near-empty launches (bench.py
+    # times only the regular rounds): dispatches >= a quarter of the median
+    if iv:
+        med = sorted(b - a for a, b in iv)[len(iv) // 2]
+        reg = [(a, b) for a, b in iv if b - a >= 0.25 * med]
+        m = max(1, len(reg))
+        res.update({"regular_dispatches": len(reg),
+                    "regular_avg_duration_ms": round(sum(b - a for a, b in reg) / m / 1e6, 4),
+                    "regular_busy_ms_per_dispatch": round(union(reg) / m / 1e6, 4)})
+    return res
 
 
 if __name__ == "__main__":
