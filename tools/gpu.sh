@@ -16,7 +16,8 @@
 #                                  for bit with the first variant's
 #   stamps NAME VARIANT [VAR=val]  tools/nn_stamps.py with abv/VARIANT (built with -DOAMD_STAMPS)
 #   benchvar NAME [bench args]     bench line of every prebuilt variant, ROUNDS interleaved sweeps
-# Every step runs under its own time limit; the first failing step ends the run
+# Trace post-processing: tools/kt_gaps.py (gaps between ResNet launches), tools/round_profile.py
+# (a step split by round). Every step runs under its own time limit; the first failing step ends the run
 # (no retries). Summaries: python tools/prof_summary.py (in the build container).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
