@@ -60,6 +60,60 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PUBLISHED_SIMS_PER_S = 28000.0
 
 
+# the sources each kernel's committed PMC traffic record was measured on
+# (profiles/traffic_*.json carry this hash; a record of other code is not used)
+KERNEL_SOURCES = {
+    "resnet": ["resnet.hip", "kernels.h"],
+    "tree": ["tree.hip", "engine.h", "bitboard.h", "rng.h", "kernels.h"],
+}
+
+
+def kernel_hash(kind: str) -> str:
+    """sha256 (16 hex digits) over the HIP sources of one kernel family."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES[kind]:
+        h.update(name.encode())
+        h.update((ROOT / "othello-alphazero_amd" / "csrc" / name).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def pipeline_groups(args) -> int:
+    """Pipeline groups of the native search (capi.hip plan_groups)."""
+    k = args.pipeline if args.pipeline > 0 else (2 if args.games >= 64 else 1)
+    return max(1, min(k, args.games, 8))
+
+
+def single_game_split(args) -> bool:
+    """One game, T > 1: the thread-split schedule (capi.hip oamd_engine_search)."""
+    return args.games == 1 and pipeline_groups(args) == 1 and 1 < args.threads <= 8
+
+
+def search_rounds(args) -> int:
+    """NN rounds of one native search (capi.hip search_rounds): one per batch of
+    a thread, plus the chain-splitting extra rounds (exact interleaving only)."""
+    steps = (args.sims + args.threads * args.batch - 1) // (args.threads * args.batch)
+    extra = args.chain_cuts if (not args.round_robin_endgames and args.chain_budget > 0
+                                and not single_game_split(args)) else 0
+    return steps + extra
+
+
+def timed_region_resnet_launches(args) -> int:
+    """k_resnet dispatches of the timed region (all rounds of every search): the
+    trace cross-check (tools/prof_summary.py) takes the last this many."""
+    if single_game_split(args):
+        return args.steps * search_rounds(args) * args.threads
+    K = pipeline_groups(args)
+    L = args.threads * args.batch
+    n = 0
+    for k in range(K):
+        grows = (args.games * (k + 1) // K - args.games * k // K) * L
+        cb = args.eval_batch if args.eval_batch > 0 else grows
+        n += (grows + cb - 1) // cb
+    return args.steps * search_rounds(args) * n
+
+
 def resnet_flops_per_eval(in_ch: int, C: int, R: int, hidden: int) -> float:
     conv0 = 2 * 64 * 9 * in_ch * C
     tower = 2 * R * 2 * 64 * 9 * C * C
@@ -178,19 +232,26 @@ def shard_seeds(seed: int, rank: int) -> tuple[int, int]:
     return seed + 7919 * rank, seed + rank
 
 
+def grouped() -> bool:
+    """True when this rank runs in a process group (every launcher run, world 1
+    included: the barrier, the MAX reduction and the rank table then go
+    through the job's backend, RCCL on the GPU box)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def timed_max(world: int, run, sync, device: str) -> float:
     """Run `run()` bracketed by barrier + device sync on both sides; return the
     MAX wall time over ranks (the whole job's time)."""
-    if world > 1:
+    if grouped():
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     run()
     sync()
-    if world > 1:
+    if grouped():
         dist.barrier()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
-    if world > 1:
+    if grouped():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -199,7 +260,7 @@ def rank_table(world: int, rank: int, device_id: str, sims: int) -> list[dict]:
     """[{rank, device, sims}] of every rank (all_gather_object over the job's
     process group): which physical device each rank ran on and its units."""
     me = {"rank": rank, "device": device_id, "sims": sims}
-    if world == 1:
+    if not grouped():
         return [me]
     out: list = [None] * world
     dist.all_gather_object(out, me)
@@ -282,6 +343,9 @@ def parse_args(argv: list[str]):
                     help="timed moves of the CPU baseline (0 = skip it), after 2 warm-up moves")
     ap.add_argument("--cpu-baseline-threads", type=int, default=0,
                     help="torch threads of the CPU baseline (0 = every CPU this process may use)")
+    ap.add_argument("--sustained-moves", type=int, default=64,
+                    help="after the timed region, continue the same games this many more moves (endgames, "
+                         "restarts) and report them as the line's `sustained` sub-record (0 = skip)")
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
     ap.add_argument("--per-move-calls", action="store_true",
@@ -327,7 +391,7 @@ def main(argv: list[str] | None = None) -> None:
     # devices round-robin, timing reduced over gloo); the driver's runs use RCCL
     backend = "gloo" if args.dry_run else os.environ.get("OAMD_BENCH_BACKEND", "nccl")
     if args.dry_run:
-        if world > 1:
+        if under_launcher():
             dist.init_process_group("gloo")
         return report(args, world, rank, backend, DryWorkload(args, rank, local))
     if backend == "gloo":
@@ -336,7 +400,10 @@ def main(argv: list[str] | None = None) -> None:
         raise SystemExit(f"bench.py: rank {rank} (local {local}) has no GPU: "
                          f"{torch.cuda.device_count()} visible")
     torch.cuda.set_device(local)
-    if world > 1:
+    # under a launcher the rank joins the job's process group at every world
+    # size (torchrun --nproc-per-node 1 runs the RCCL init, barrier, MAX
+    # all-reduce and rank table too); a bare world-1 run has none
+    if under_launcher():
         if backend == "gloo":
             dist.init_process_group("gloo")
         else:
@@ -390,9 +457,9 @@ class EngineWorkload:
     def sync(self) -> None:
         torch.cuda.synchronize()
 
-    def start_measuring(self) -> None:
+    def start_measuring(self, every: int | None = None) -> None:
         e = self.b.engine
-        e.enable_timing(max(1, self.args.timing_every))
+        e.enable_timing(max(1, self.args.timing_every if every is None else every))
         self.t0 = (e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy())
 
     def stop_measuring(self) -> dict:
@@ -430,6 +497,17 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
 
     dt_max = timed_max(world, run, wl.sync, "cuda" if backend == "nccl" else "cpu")
     m = wl.stop_measuring() if measuring else None
+    sustained = None
+    if measuring and args.sustained_moves > 0:
+        # the engine's real workload: the same games played on through their
+        # endgames (all-terminal batches, chain splitting) and restarts. Every
+        # search is timed: the work per search varies with the games' phase
+        # (the games start together, so their endgames coincide) and a
+        # 1-in-5 sample is biased (~1 % event cost)
+        wl.start_measuring(1)
+        dt_s = timed_max(world, lambda: steps(args.sustained_moves), wl.sync,
+                         "cuda" if backend == "nccl" else "cpu")
+        sustained = sustained_fields(args, wl.stop_measuring(), world, sims_per_search, dt_s)
     value = aggregate_rate(world, args.games, sims_per_search, args.steps, dt_max)
     ranks = rank_table(world, rank, wl.device_id, args.games * sims_per_search * args.steps)
     check_ranks(args, world, backend, ranks)
@@ -466,7 +544,7 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
                             + (" (REHEARSAL: ranks share GPUs; not a scaling point)"
                                if n_devices < world else "")),
             "ranks": ranks,
-            "backend": (backend if world > 1 else "none"),
+            "backend": (backend if grouped() else "none"),
             "endgame_interleaving": ("round-robin" if args.round_robin_endgames else
                                      f"exact (reference), chains split after {args.chain_budget} re-selections, "
                                      f"<= {args.chain_cuts} times per search"),
@@ -478,14 +556,55 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
         result["dry_run"] = True
     if m is not None:
         result.update(measured_fields(args, m, workload))
+        if sustained is not None:
+            result["sustained"] = sustained
         if rank == 0 and world == 1 and args.cpu_baseline_moves > 0:
             result["cpu_baseline"] = cpu_baseline(args.history, args.channels, args.blocks - 1, args.hidden,
                                                   moves=args.cpu_baseline_moves,
                                                   threads=args.cpu_baseline_threads or None)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if grouped():
         dist.destroy_process_group()
+
+
+def sustained_fields(args, m: dict, world: int, sims_per_search: int, dt_max: float) -> dict:
+    """The `sustained` sub-record: `sustained_moves` more moves of the same
+    games right after the timed region (not part of `value`)."""
+    import copy
+
+    n = args.sustained_moves
+    a = copy.copy(args)
+    a.steps = n  # the record's own moves (rows launched, timed-region launches)
+    mf = measured_fields(a, m, "")
+    r = mf["roofline"]
+    return {
+        "moves": n,
+        "value": round(aggregate_rate(world, args.games, sims_per_search, n, dt_max), 1),
+        "unit": "simulations/s",
+        "ms_per_step": round(dt_max * 1e3 / n, 3),
+        "work": mf["work"],
+        "note": (f"the same {args.games} games per GPU continued for {n} moves after the timed region "
+                 "(endgames with the reference's interleaving, restarts from random openings)"),
+        "roofline": {k: r[k] for k in ("achieved", "peak", "unit", "frac", "avg_launch_ms", "busy_ms_per_launch",
+                                       "rows_per_launch", "n_eval_per_launch", "timed_region_launches")},
+        "tree_kernels": mf["tree_kernels"],
+    }
+
+
+def traffic_record(name: str, kind: str, workload: str) -> dict | None:
+    """A committed PMC traffic summary (profiles/NAME), if it was measured on
+    this workload and on the current sources of the kernel family `kind`."""
+    f = ROOT / "profiles" / name
+    if not f.exists():
+        return None
+    try:
+        tj = json.loads(f.read_text())
+    except (ValueError, OSError):
+        return None
+    if tj.get("workload") != workload or tj.get("kernel_hash") != kernel_hash(kind):
+        return None
+    return tj
 
 
 def measured_fields(args, m: dict, workload: str) -> dict:
@@ -505,8 +624,10 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     rows_launched = args.games * args.threads * args.batch * ((args.sims + args.threads * args.batch - 1)
                                                               // (args.threads * args.batch)) * args.steps
     eval_share = m["evals"] / max(1, rows_launched)
-    # the timed searches' own NN rows (device counters of exactly the timed
-    # rounds; the chain-splitting extra rounds' small launches are not timed)
+    # the timed searches' own NN rows (device counters of every round of the
+    # timed searches, the chain-splitting extra rounds included), over those
+    # searches' launches, all rounds: rows, launches and busy time cover the
+    # same launches
     n_eval_per_launch = m["timed_evals"] / max(1, m["nn_launches"])
     achieved = flops * n_eval_per_launch / (busy_ms * 1e-3) / 1e12
     # every launched row counted as work (the round-2 basis): n_eval / eval_share
@@ -514,32 +635,25 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     executed = flops - 2.0 * 64 * 9 * args.channels * args.channels * 2 * R // 12
     peak = PEAK_TFLOPS[args.dtype]
     # HBM bytes per launch from the committed PMC summary of this same workload
+    # AND the same kernel sources (kernel_hash)
     traffic = None
-    tfile = ROOT / "profiles" / "traffic_resnet.json"
-    if tfile.exists():
-        try:
-            tj = json.loads(tfile.read_text())
-            if tj.get("workload") == workload and tj.get("rows_per_launch") == int(rows_per_launch):
-                traffic = tj.get("bytes_per_launch")
-        except (ValueError, OSError):
-            traffic = None
+    tj = traffic_record("traffic_resnet.json", "resnet", workload)
+    if tj and tj.get("rows_per_launch") == int(rows_per_launch):
+        traffic = tj.get("bytes_per_launch")
     tree_bytes = {}
-    tfile = ROOT / "profiles" / "traffic_tree.json"
-    if tfile.exists():
+    tj = traffic_record("traffic_tree.json", "tree", workload)
+    if tj:
         try:
-            tj = json.loads(tfile.read_text())
-            if tj.get("workload") == workload and tj.get("rows_per_launch") == int(rows_per_launch):
-                tree_bytes = {k: v["bytes_per_launch"] for k, v in tj["kernels"].items()}
-        except (ValueError, OSError, KeyError):
+            tree_bytes = {k: v["bytes_per_launch"] for k, v in tj["kernels"].items()}
+        except (KeyError, TypeError):
             tree_bytes = {}
     # k_tree: one launch per search round and pipeline group; "select" rounds
     # back up the previous batch and select the next, the final round backs up
-    tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch)}
-    steps_per_search = (args.sims + args.threads * args.batch - 1) // (args.threads * args.batch)
-    # timed rounds per search: the batches per thread (the chain-splitting
-    # extra rounds carry no events) + the final backup
+    tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch), "rounds_per_search": search_rounds(args)}
+    # timed rounds per search: every selecting round (the chain-splitting extra
+    # rounds included) + the final backup
     for name, ms, n in (("k_tree", m["select_ms"], m["tree_launches"]),
-                        ("k_tree_final_backup", m["backup_ms"], m["tree_launches"] // steps_per_search)):
+                        ("k_tree_final_backup", m["backup_ms"], m["tree_launches"] // search_rounds(args))):
         avg = ms / max(1, n)
         entry = {"avg_launch_ms": round(avg, 4)}
         if name in tree_bytes:
@@ -559,9 +673,11 @@ def measured_fields(args, m: dict, workload: str) -> dict:
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
-            "basis": ("n_eval rows (the timed searches' non-terminal leaves) per launch x flops_per_row / busy "
-                      "ms per launch (the union of the timed launch intervals / launches; = avg_launch_ms when "
-                      "launches do not overlap)"),
+            "basis": ("n_eval rows (the timed searches' non-terminal leaves, every round) per launch x "
+                      "flops_per_row / busy ms per launch (the union of the timed searches' launch intervals, "
+                      "every round, / their launches; = avg_launch_ms when launches do not overlap)"),
+            "timed_region_launches": timed_region_resnet_launches(args),
+            "kernel_hash": kernel_hash("resnet"),
             "avg_launch_ms": round(avg_ms, 4),
             "busy_ms_per_launch": round(busy_ms, 4),
             "nn_chains": args.nn_chains,

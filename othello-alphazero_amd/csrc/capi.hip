@@ -17,6 +17,7 @@
 
 #include "engine.h"
 #include "kernels.h"
+#include "timing.h"
 
 using namespace oamd;
 
@@ -240,18 +241,7 @@ struct oamd_engine {
                 iv.emplace_back(t0, t1);
             }
         }
-        std::sort(iv.begin(), iv.end());
-        float lo = 0.0f, hi = -1.0f;
-        for (const auto& x : iv) {
-            if (x.first > hi) {
-                if (hi > lo) nn_busy_ms += hi - lo;
-                lo = x.first;
-                hi = x.second;
-            } else if (x.second > hi) {
-                hi = x.second;
-            }
-        }
-        if (hi > lo) nn_busy_ms += hi - lo;
+        nn_busy_ms += (float)interval_union(iv);
         nn_launches += ev_launches[p];
         tree_launches += ev_final[p];
         nn_rows += ev_rows[p];
@@ -954,8 +944,19 @@ static GroupPlan plan_groups(oamd_engine* e) {
     return P;
 }
 
+// Extra rounds of a native grouped search (chain splitting, k_tree): the
+// reference's interleaving only
+static int extra_rounds(const oamd_engine* e) {
+    return e->exact_interleaving && e->chain_budget > 0 ? e->chain_cuts : 0;
+}
+
+// Selecting rounds (= NN rounds) of a native grouped search: one per batch of
+// a thread plus the chain-splitting extra rounds
+static int search_rounds(const oamd_engine* e, int steps) { return steps + extra_rounds(e); }
+
 // Sampled timing of one search: claim the current event pool (every
-// timing_stride-th search), sized for NB blocks per round.
+// timing_stride-th search), sized for NB blocks per round and `steps` NN
+// rounds (search_rounds) plus the final backup-only round.
 static int timing_begin(oamd_engine* e, int steps, int NB, bool* timed) {
     *timed = e->timing && (e->search_count++ % e->timing_stride) == 0;
     if (!*timed) return OAMD_OK;
@@ -994,11 +995,6 @@ static void timing_end(oamd_engine* e, int steps, int NB, bool split, const Grou
 // streams (already forked from the engine stream). chained: the groups'
 // streams carry on from a previous search of the same call (a multi-move
 // self-play call), so its first NN launch also waits for the NN token.
-// Extra rounds of a native grouped search (chain splitting, k_tree): the
-// reference's interleaving only
-static int extra_rounds(const oamd_engine* e) {
-    return e->exact_interleaving && e->chain_budget > 0 ? e->chain_cuts : 0;
-}
 
 static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPlan& P, int steps, bool timed,
                                 bool chained) {
@@ -1015,22 +1011,21 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
     // rounds 0..S (k_tree): round s backs up what the previous rounds selected
     // and selects, thread by thread; the NN evaluates round s's selections
     // between rounds s and s+1; the last round only backs up. A timed search
-    // records events for rounds 0..steps-1 and the last one, and counts the
-    // work of rounds 0..steps-1 (counters [4..5]): the extra rounds' small
-    // launches (lagging games only) are left out of both
+    // records events for every round, the extra ones included, and counts the
+    // NN rows of every round (counters [4..5]): launches, rows and busy time
+    // of a timed search cover the same launches (search_rounds)
     for (int s = 0; s <= S; ++s) {
-        const int blk = s < steps ? s : (s == S ? steps : -1);
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)P.g0[k] * L;
             hipStream_t sk = P.st[k];
-            hipEvent_t* ev = timed && blk >= 0 ? &e->ev[pool][kEvPerBlock * (blk * K + k)] : nullptr;
+            hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
             if (ev) HIPCHK(hipEventRecord(ev[0], sk));
             // evaluation list of group k: round s fills counter s % 2 and zeroes
             // the other one (which round s-1's launch, done by now, read); the
             // final round zeroes counter 0 for the next search's round 0
             int* cnt = e->rowcount + 2 * k;
             launch_tree(E, sk, s > 0, s < S, T, B, P.g0[k], P.ng[k], 0, -1, s < S ? cnt + (s & 1) : nullptr,
-                        s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X, timed && s < steps);
+                        s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X, timed);
             if (ev) HIPCHK(hipEventRecord(ev[1], sk));
             if (s == S) continue;
             // the groups' NN launches run one after another (OAMD_NN_ORDER)
@@ -1104,7 +1099,8 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     // sampled timing: per (round, group) kEvPerBlock events: tree begin/end, NN
     // begin/end (on the NN stream, after its waits; not in the final round)
     bool timed = false;
-    if ((rc = timing_begin(e, steps, NB, &timed))) return rc;
+    const int rounds = split ? steps : search_rounds(e, steps);  // NN rounds
+    if ((rc = timing_begin(e, rounds, NB, &timed))) return rc;
     const int pool = e->ev_cur;
     for (int s = 0; split && s <= steps; ++s) {
         for (int t = 0; t < T; ++t) {
@@ -1130,7 +1126,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     }
     LAUNCHCHK();
     if (!split && (rc = join_groups(e, P))) return rc;
-    if (timed) timing_end(e, steps, NB, split, P);
+    if (timed) timing_end(e, rounds, NB, split, P);
     // without counters requested the search is left in flight (stream order)
     if (sims || evals) {
         unsigned long long c[2] = {0, 0};
@@ -1333,12 +1329,12 @@ int oamd_engine_selfplay_steps(oamd_engine* e, oamd_net* net, const oamd_selfpla
     int rc = fork_groups(e, P);
     for (int i = 0; !rc && i < n_moves; ++i) {
         bool timed = false;
-        if ((rc = timing_begin(e, steps, P.K, &timed))) break;
+        if ((rc = timing_begin(e, search_rounds(e, steps), P.K, &timed))) break;
         if ((rc = enqueue_group_rounds(e, N, P, steps, timed, i > 0))) break;
         for (int k = 0; k < P.K; ++k)
             launch_selfplay_move(E, sp, P.g0[k], P.ng[k], out(i, actions_dev, 1), out(i, finished_dev, 1),
                                  out(i, features_dev, 8 * C * 64), out(i, policy_dev, 8 * 65), P.st[k]);
-        if (timed) timing_end(e, steps, P.K, false, P);
+        if (timed) timing_end(e, search_rounds(e, steps), P.K, false, P);
     }
     if (rc) return rc;
     LAUNCHCHK();

@@ -55,6 +55,12 @@ struct GameState {
 // bits 8..10 = transform, bit 16 = row valid (non-terminal leaf).
 __host__ __device__ inline int feature_words(int H) { return 2 + 2 * H; }
 
+// k_tree per-thread state (EngineView::tstate): batches selected in this search
+// in the low 31 bits (steps = ceil(S / L) has no upper limit), the batch
+// waiting for the NN in bit 31
+constexpr int32_t kTstateSel = 0x7FFFFFFF;
+constexpr int32_t kTstatePend = (int32_t)0x80000000u;
+
 struct EngineView {
     int32_t G, L, H, FW;
     int64_t cap;
@@ -73,7 +79,7 @@ struct EngineView {
     float c_base, c_init, eps, alpha;
     unsigned long long* counters;  // [0] sims, [1] evals (this search), [2] sims, [3] evals (cumulative)
     int32_t* rowlist;  // G*L: evaluation lists (pipeline group k: from its first game's row)
-    int32_t* tstate;   // G*L (entry g*L + t for virtual thread t): batches selected | pending << 16
+    int32_t* tstate;   // G*L (entry g*L + t for virtual thread t): batches selected | kTstatePend
     int32_t steps;     // batches per virtual thread and search: ceil(num_simulations / L)
     int32_t B;         // batch_size (leaves per virtual thread and batch)
     int32_t terminal_skip;  // 1: an all-terminal batch is backed up at once and its thread selects

@@ -523,15 +523,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     int cut_at = -1;   // the thread whose chain this round stopped
     // a search's first round starts every thread fresh, also the ones a split
     // chain keeps it from visiting (their state is read from the next round on)
-    if (fresh && budget > 0 && lane < nt) E.tstate[(size_t)g * E.L + t0 + lane] = 0;
+    // (strided: a search may run up to 1024 virtual threads)
+    if (fresh && budget > 0)
+        for (int t = t0 + lane; t < t1; t += 64) E.tstate[(size_t)g * E.L + t] = 0;
     for (int k = 0; k < nt && cut_at < 0; ++k) {
         const int t = t0 + (rp - t0 + k) % nt;
         // virtual thread t: batches selected so far in this search, and whether
         // its last batch waits for the NN (a search's first round starts fresh)
         int* ts = E.tstate + (size_t)g * E.L + t;
         const int st = fresh ? 0 : *ts;
-        int sel = st & 0xFFFF;
-        bool pend = (st >> 16) & 1;
+        int sel = st & kTstateSel;
+        bool pend = (st & kTstatePend) != 0;
         if (do_backup && pend) {
             backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
             pend = false;
@@ -558,7 +560,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
                 ++chain;
             }
         }
-        if (lane == 0) *ts = sel | (pend ? 1 << 16 : 0);
+        if (lane == 0) *ts = sel | (pend ? kTstatePend : 0);
     }
     if (lane == 0) {
         if (budget > 0) {
@@ -624,7 +626,7 @@ __global__ __launch_bounds__(256) void k_leaf_flags(EngineView E, uint8_t* flags
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r >= E.G * E.L) return;
     const int g = r / E.L, t = (r % E.L) / E.B;
-    const bool pend = (E.tstate[(size_t)g * E.L + t] >> 16) & 1;
+    const bool pend = (E.tstate[(size_t)g * E.L + t] & kTstatePend) != 0;
     flags[r] = (uint8_t)(pend && ((E.feat[(size_t)r * E.FW] >> 16) & 1ULL));
 }
 

@@ -34,6 +34,8 @@ DRIVER = ROOT / "oracle" / "_ref" / "ref_driver"
 REF_PY = Path("/root/reference/python")
 
 sys.path.insert(0, str(ROOT / "othello-alphazero_amd"))
+sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "tests"))
 
 
 def run(*args: str) -> list[str]:
@@ -159,24 +161,13 @@ def make_strings_errors() -> None:
 
 
 def _real_features(n: int, history_size: int, seed: int) -> np.ndarray:
-    """Feature planes of real positions (oracle restatement, pinned above)."""
+    """Feature planes of real positions (oracle restatement, pinned above;
+    tests/ref_fixtures.py:real_features, which the GPU tests re-run)."""
     sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle as O
+    sys.path.insert(0, str(ROOT / "tests"))
+    from ref_fixtures import real_features
 
-    rng = np.random.default_rng(seed)
-    out = []
-    for _ in range(n):
-        chain = [O.initial_position()]
-        for _ in range(int(rng.integers(0, 58))):
-            p = chain[-1]
-            if p.player == 0:
-                break
-            acts = O.legal_actions(p)
-            chain.append(O.apply_action(p, int(acts[rng.integers(len(acts))])))
-        if chain[-1].player == 0:
-            chain.pop()
-        out.append(O.features(chain[::-1], history_size, int(rng.integers(8))))
-    return np.stack(out).astype(np.float32)
+    return real_features(n, history_size, seed)
 
 
 def make_resnet() -> None:
@@ -217,6 +208,46 @@ def make_resnet() -> None:
     (GOLD / "resnet_meta.json").write_text(json.dumps(meta, indent=1))
 
 
+def make_resnet_large() -> None:
+    """The throughput geometries (>= 1024 rows per launch: 4-board C=128
+    workgroups, the register-queue C=256 ones) against the reference's own
+    AlphaZeroNet. Only (seed, rows) and a checksum of the planes are stored;
+    tests/test_gpu_resnet.py regenerates the planes (ref_fixtures.real_features)."""
+    import torch
+
+    sys.path.insert(0, str(REF_PY))
+    from othello_alphazero.neural_net import AlphaZeroNet  # reference, read-only
+
+    from othello_mcts.synthetic import alphazero_state_dict, net_config_from_state_dict
+    from ref_fixtures import planes_checksum
+
+    torch.set_num_threads(8)
+    cases = {
+        # name: (weight seed, H, C, blocks, hidden, rows, planes seed); rows ragged
+        # in the last workgroup (4 boards at C=128, 2 at C=256)
+        "c128b9_h8_r1027": (1235, 8, 128, 9, 128, 1027, 71),
+        "c128b9_h4_r1029": (4322, 4, 128, 9, 128, 1029, 72),
+        "c256b19_h8_r1025": (2028, 8, 256, 19, 256, 1025, 73),
+    }
+    meta, arrays = {}, {}
+    for name, (seed, H, C, R, hid, n, xseed) in cases.items():
+        sd = alphazero_state_dict(seed, 1 + 2 * H, C, R, hid)
+        net = AlphaZeroNet(**net_config_from_state_dict(sd))
+        net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+        net.eval()
+        x = _real_features(n, H, xseed)
+        with torch.no_grad():
+            out = net(torch.from_numpy(x))
+        arrays[f"{name}_policy"] = out["policy"].numpy()
+        arrays[f"{name}_value"] = out["value"].numpy()
+        meta[name] = {"seed": seed, "history_size": H, "conv_channels": C, "num_residual_blocks": R,
+                      "value_head_hidden_channels": hid, "boards": n, "planes_seed": xseed,
+                      "planes_sha256_16": planes_checksum(x)}
+        print("resnet large", name, "rows", n, "value[0]", float(out["value"][0]))
+    np.savez_compressed(GOLD / "resnet_large.npz", **arrays)
+    (GOLD / "resnet_large_meta.json").write_text(json.dumps(meta, indent=1))
+
+
 def make_mcts_known_answers() -> None:
     data = {
         "provenance": "SURVEY.md section 4 (measured with the compiled reference extension)",
@@ -233,9 +264,13 @@ def make_mcts_known_answers() -> None:
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["resnet_large"]:
+        make_resnet_large()
+        raise SystemExit(0)
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "ref", "all"], check=True)
     make_bitboards()
     make_features()
     make_strings_errors()
     make_resnet()
+    make_resnet_large()
     make_mcts_known_answers()

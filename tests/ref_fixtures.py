@@ -19,6 +19,38 @@ import numpy as np
 GOLD = Path(__file__).resolve().parent / "golden"
 
 
+def real_features(n: int, history_size: int, seed: int) -> np.ndarray:
+    """Feature planes of `n` real positions: seeded random games from the
+    initial position (0-57 plies), each with its history and a random D4
+    transform, built by the oracle restatement (pinned by the reference's
+    feature vectors, test_oracle_golden.py). The ResNet goldens are the
+    reference AlphaZeroNet's outputs on these planes (make_golden.py); the
+    large ones store only (n, seed) and a checksum of the planes, which the
+    tests regenerate here."""
+    import oracle as O
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        chain = [O.initial_position()]
+        for _ in range(int(rng.integers(0, 58))):
+            p = chain[-1]
+            if p.player == 0:
+                break
+            acts = O.legal_actions(p)
+            chain.append(O.apply_action(p, int(acts[rng.integers(len(acts))])))
+        if chain[-1].player == 0:
+            chain.pop()
+        out.append(O.features(chain[::-1], history_size, int(rng.integers(8))))
+    return np.stack(out).astype(np.float32)
+
+
+def planes_checksum(x: np.ndarray) -> str:
+    import hashlib
+
+    return hashlib.sha256(np.ascontiguousarray(x.astype(np.int8)).tobytes()).hexdigest()[:16]
+
+
 def load_cases() -> list[dict]:
     return json.loads((GOLD / "ref_mcts.json").read_text())["cases"]
 

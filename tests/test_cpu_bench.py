@@ -15,10 +15,11 @@ sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 
 
-def _m(launches=50, busy_per=0.75, span_per=1.05, rows=4096, evals_share=0.9, steps=10):
+def _m(launches=56, busy_per=0.75, span_per=1.05, rows=4096, evals_share=0.9, steps=10):
+    # one timed search, 2 pipeline groups x 28 rounds (25 + 3 chain-splitting extra rounds)
     return {"nn_ms": span_per * launches, "nn_busy_ms": busy_per * launches, "nn_launches": launches,
             "nn_rows": rows * launches, "timed_evals": int(rows * evals_share * launches),
-            "select_ms": 0.45 * 25 * 2, "backup_ms": 0.13 * 2, "tree_launches": 25 * 2,
+            "select_ms": 0.45 * 28 * 2, "backup_ms": 0.13 * 2, "tree_launches": 28 * 2,
             "sims": 256 * 800 * steps, "evals": int(256 * 800 * steps * evals_share), "overflow_games": 0}
 
 
@@ -37,7 +38,7 @@ def test_roofline_uses_union_busy_time_and_timed_rows():
     share = out["work"]["n_eval"] / out["work"]["rows_launched"]
     assert r["achieved_rows_launched"] == pytest.approx(r["achieved"] / share, rel=1e-3)
     assert out["work"]["terminal_share"] == pytest.approx(0.1, abs=1e-3)
-    # tree: 25 select rounds per search and group, one final backup each
+    # tree: 28 select rounds per search and group (3 extra), one final backup each
     t = out["tree_kernels"]
     assert t["k_tree"]["avg_launch_ms"] == pytest.approx(0.45)
     assert t["k_tree_final_backup"]["avg_launch_ms"] == pytest.approx(0.13)
@@ -47,3 +48,114 @@ def test_one_chain_union_equals_summed_durations():
     args = bench.parse_args(["--nn-chains", "1"])
     r = bench.measured_fields(args, _m(busy_per=0.8, span_per=0.8), "w")["roofline"]
     assert r["avg_launch_ms"] == r["busy_ms_per_launch"] and r["nn_chains"] == 1
+
+
+def test_rounds_and_timed_region_launches():
+    """Every round of a search is an NN round: 25 batches per thread + the
+    chain-splitting extra rounds (exact interleaving only); the timed region's
+    k_resnet dispatches are steps x groups x rounds x launches per group."""
+    a = bench.parse_args([])
+    assert bench.search_rounds(a) == 28 and bench.pipeline_groups(a) == 2
+    assert bench.timed_region_resnet_launches(a) == 10 * 2 * 28
+    a = bench.parse_args(["--round-robin-endgames"])
+    assert bench.search_rounds(a) == 25
+    a = bench.parse_args(["--chain-budget", "0", "--steps", "4"])
+    assert bench.timed_region_resnet_launches(a) == 4 * 2 * 25
+    # configs[4] shard: 2048-row launches over 512 games (2 x 8192-row groups)
+    a = bench.parse_args(["--games", "512", "--dtype", "fp16", "--eval-batch", "2048", "--steps", "3"])
+    assert bench.timed_region_resnet_launches(a) == 3 * 28 * 2 * 4
+    # configs[3]: 1600 sims = 50 batches per thread
+    a = bench.parse_args(["--sims", "1600", "--channels", "256", "--blocks", "20"])
+    assert bench.search_rounds(a) == 53
+    # one game, T > 1: the thread-split schedule has no extra rounds
+    a = bench.parse_args(["--games", "1"])
+    assert bench.single_game_split(a) and bench.search_rounds(a) == 25
+    assert bench.timed_region_resnet_launches(a) == 10 * 25 * 2
+
+
+def test_n_eval_per_launch_within_launched_rows_with_extra_rounds():
+    """With extra rounds present (near-empty launches for lagging games) the
+    rows per launch still cover every launch of the timed searches: n_eval per
+    launch <= rows per launch x (1 - terminal share)."""
+    args = bench.parse_args(["--steps", "10"])
+    # 2 timed searches: 2 x 2 x 28 launches of 4096-row capacity; the regular
+    # rounds hold 0.9 of the rows as non-terminal, the extra rounds 2 %
+    launches = 2 * 2 * 28
+    timed = int(2 * 2 * (25 * 4096 * 0.9 + 3 * 4096 * 0.02))
+    m = _m(launches=launches)
+    m["timed_evals"] = timed
+    m["evals"] = int(timed * 5)  # every 5th search timed
+    m["sims"] = 256 * 800 * 10
+    out = bench.measured_fields(args, m, "w")
+    r = out["roofline"]
+    share = out["work"]["terminal_share"]
+    assert r["n_eval_per_launch"] <= r["rows_per_launch"] * (1 - share) + 1e-6
+    assert r["timed_region_launches"] == 10 * 2 * 28
+    assert len(r["kernel_hash"]) == 16
+
+
+def _timing_lib(tmp_path):
+    src = tmp_path / "u.cpp"
+    src.write_text('''#include "timing.h"
+#include <cstdio>
+extern "C" double iu(const float* a, int n) {
+    std::vector<std::pair<float, float>> v;
+    for (int i = 0; i < n; ++i) v.emplace_back(a[2 * i], a[2 * i + 1]);
+    return interval_union(v);
+}
+''')
+    so = tmp_path / "u.so"
+    import subprocess
+
+    subprocess.run(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-I", str(ROOT / "othello-alphazero_amd" / "csrc"),
+                    str(src), "-o", str(so)], check=True)
+    import ctypes
+
+    lib = ctypes.CDLL(str(so))
+    lib.iu.restype = ctypes.c_double
+    lib.iu.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+
+    def iu(pairs):
+        import numpy as np
+
+        a = np.ascontiguousarray(np.asarray(pairs, dtype=np.float32).reshape(-1))
+        return lib.iu(a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), len(pairs))
+    return iu
+
+
+def test_interval_union_of_the_engine(tmp_path):
+    """csrc/timing.h: the busy time of overlapping NN chains. Intervals are
+    measured from group 0's first event and another group's stream may run
+    ahead of it (negative starts, more than 1 ms before): the union keeps them
+    whole (ADVICE r3: a sweep anchored at 0 cut them)."""
+    import random
+
+    sys.path.insert(0, str(ROOT / "tools"))
+    from prof_summary import interval_union as py_union
+
+    iu = _timing_lib(tmp_path)
+    assert iu([]) == 0.0
+    assert iu([(-3.0, -2.0)]) == pytest.approx(1.0)
+    assert iu([(-3.0, -1.5), (-2.0, 0.5), (1.0, 2.0)]) == pytest.approx(4.5)
+    assert iu([(0.0, 4.0), (1.0, 2.0), (3.0, 5.0)]) == pytest.approx(5.0)
+    rng = random.Random(3)
+    for _ in range(200):
+        xs = []
+        for _ in range(rng.randint(1, 40)):
+            a = rng.uniform(-20, 20)
+            xs.append((a, a + rng.uniform(0, 3)))
+        assert iu(xs) == pytest.approx(py_union(xs), abs=1e-4)
+
+
+def test_sustained_record_uses_its_own_moves():
+    """The `sustained` sub-record (moves after the timed region): its rate,
+    rows launched and timed-region launches count its own moves."""
+    args = bench.parse_args(["--steps", "10", "--sustained-moves", "64"])
+    m = _m()
+    m["sims"] = 256 * 800 * 64
+    m["evals"] = int(m["sims"] * 0.85)
+    out = bench.sustained_fields(args, m, 1, 800, 2.56)
+    assert out["moves"] == 64 and out["value"] == pytest.approx(256 * 800 * 64 / 2.56, rel=1e-6)
+    assert out["work"]["rows_launched"] == 256 * 800 * 64
+    assert out["work"]["terminal_share"] == pytest.approx(0.15, abs=1e-3)
+    assert out["roofline"]["timed_region_launches"] == 64 * 2 * 28

@@ -73,6 +73,21 @@ def test_driver_launch_gpus2():
     _check_two_rank_line(_one_line(r), 2, 25.0, 8)
 
 
+def test_driver_launch_gpus1_joins_a_process_group():
+    """Under a launcher even one rank runs the group path (on the GPU box: the
+    RCCL init, barrier, MAX all-reduce and rank table of an N=1 run)."""
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+              "--master-addr=127.0.0.1", f"--master-port={_free_port()}", BENCH,
+              "--gpus", "1", "--dry-run", "--steps", "2", "--warmup", "0", "--games", "4", "--dry-step-ms", "10"])
+    out = _one_line(r)
+    assert out["n_gpus"] == 1 and out["config"]["backend"] == "gloo"
+    assert [x["rank"] for x in out["config"]["ranks"]] == [0]
+    # a bare world-1 run has no process group
+    out = _one_line(_run([sys.executable, BENCH, "--dry-run", "--steps", "1", "--warmup", "0", "--games", "4",
+                          "--dry-step-ms", "5"]))
+    assert out["config"]["backend"] == "none"
+
+
 def test_ranks_must_match_gpus():
     r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", BENCH,

@@ -6,7 +6,8 @@ configs[1]: 256 games, 128x10b bf16, H=8, T=2 x B=16, 800 sims/move: the bench
             NativeNet, 8192 rows per call): identical visit counts and Q for all
             256 games; the schedule's simulation count; no pool overflow; 64
             sampled rows of a real 4096-row launch vs the fp32 restatement.
-configs[3]: 256x20b, 1600 sims/move: the same properties on 8 games.
+configs[3]: 256x20b, 1600 sims/move: the same properties at the benched shape
+            (256 games, C=256 throughput geometry).
 configs[4]: the per-GPU shard of 4096 games over 8 GPUs = 512 games, fp16,
             eval batch 2048 (oamd_engine_set_nn_batch): identical to whole-group
             launches for all 512 games, no overflow.
@@ -61,19 +62,15 @@ def _check_search(om, sd, dtype, G, H, sims, seed, name):
     return net, a
 
 
-def test_configs1_full_shape(om):
-    from othello_mcts.synthetic import alphazero_state_dict
-
-    sd = alphazero_state_dict(2025, 17, 128, 9, 128)
-    net, a = _check_search(om, sd, "bf16", 256, 8, 800, 11, "configs[1]")
-    # a real 4096-row launch: the rows one pipeline group evaluates in a step
-    b = _engine(om, 256, 8, 800, 12)
-    b.search(net)
+def _sampled_launch_rows(om, net, sd, b, G, C_in, dtype, name):
+    """A real 4096-row launch (the rows one pipeline group evaluates in a step,
+    after a move with tree reuse): 64 sampled non-terminal rows vs the fp32
+    restatement (oracle/resnet_ref.py)."""
     b.selfplay_move(temperature_moves=12, opening_moves=0)
     b.engine.search_begin()
     b.engine.select()
-    feat = torch.empty((256 * 32, 17, 8, 8), dtype=torch.float32, device=DEV)
-    b.engine.features(feat.data_ptr(), 0, 256 * 32)
+    feat = torch.empty((G * 32, C_in, 8, 8), dtype=torch.float32, device=DEV)
+    b.engine.features(feat.data_ptr(), 0, G * 32)
     x = feat[:4096].contiguous()
     flags = torch.from_numpy(b.engine.leaf_flags()[:4096].astype(bool))
     out = net(x)
@@ -85,17 +82,33 @@ def test_configs1_full_shape(om):
     ref = resnet_ref.forward(sd_t, xs)
     dp = (out["policy"][pick.to(DEV)].cpu() - ref["policy"]).abs().max().item()
     dv = (out["value"][pick.to(DEV)].cpu() - ref["value"]).abs().max().item()
-    numerics.record("configs[1] 4096-row launch, 64 sampled rows", f"max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e}")
+    numerics.record(f"{name} 4096-row launch, 64 sampled rows", f"max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e}")
     assert len(pick) == 64
-    assert dp <= TOL["bf16"][0] and dv <= TOL["bf16"][1]
+    assert dp <= TOL[dtype][0] and dv <= TOL[dtype][1]
     b.engine.backup()
 
 
-def test_configs3_shape(om):
+def test_configs1_full_shape(om):
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    sd = alphazero_state_dict(2025, 17, 128, 9, 128)
+    net, a = _check_search(om, sd, "bf16", 256, 8, 800, 11, "configs[1]")
+    b = _engine(om, 256, 8, 800, 12)
+    b.search(net)
+    _sampled_launch_rows(om, net, sd, b, 256, 17, "bf16", "configs[1]")
+
+
+def test_configs3_benched_shape(om):
+    """configs[3] at the shape the bench runs it (256 games of 256x20b, 1600
+    sims/move): 4096-row launches in the C=256 throughput geometry, whose
+    register-queue weight stream crosses all 39 conv layers. Native ==
+    callback for every game, no pool overflow, and 64 rows of a real launch vs
+    the fp32 restatement."""
     from othello_mcts.synthetic import alphazero_state_dict
 
     sd = alphazero_state_dict(2026, 17, 256, 19, 256)
-    _check_search(om, sd, "bf16", 8, 8, 1600, 21, "configs[3]")
+    net, a = _check_search(om, sd, "bf16", 256, 8, 1600, 21, "configs[3]")
+    _sampled_launch_rows(om, net, sd, a, 256, 17, "bf16", "configs[3]")
 
 
 def test_configs4_shard(om):
@@ -310,3 +323,54 @@ def test_chain_split_keeps_every_game_identical(om):
     numerics.record("chain split", f"64 late games x 24 moves: terminal-leaf share {share:.3f}, "
                                    "budgets 0/1/4 == callback")
     assert share > 0.1
+
+
+def test_chain_split_with_more_than_64_threads(om):
+    """T = 128 virtual threads (one wave serves them in turn): a chain split in
+    a search's first round leaves threads unvisited, and every one of them
+    must still start the search fresh (k_tree resets the per-thread state with
+    a strided loop). Late games, budget 1: the split search equals
+    the unsplit callback path move after move."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(44, 9, 128, 1, 32), device=0)
+    kw = dict(history_size=4, num_simulations=1536, num_threads=128, batch_size=4, dirichlet_epsilon=0.25,
+              seed=18, node_capacity=1 << 18)
+    x = om.BatchedMCTS(16, **kw)
+    x.engine.set_chain_split(1, 3)
+    ref = om.BatchedMCTS(16, **kw)
+    for b in (x, ref):
+        b.random_openings(50, seed=19)
+    total_sims = total_evals = 0
+    for mv in range(8):
+        sr, er = ref.search(lambda f: net(f))
+        total_sims += sr
+        total_evals += er
+        assert x.search(net) == (sr, er), mv
+        vr, qr = ref.root_stats()
+        v, q = x.root_stats()
+        assert torch.equal(v, vr) and torch.equal(q, qr), mv
+        o = x.selfplay_move(temperature_moves=12, opening_moves=50)
+        orf = ref.selfplay_move(temperature_moves=12, opening_moves=50)
+        assert torch.equal(o["actions"], orf["actions"]) and torch.equal(o["finished"], orf["finished"]), mv
+    numerics.record("chain split T=128", f"16 late games x 8 moves: terminal-leaf share "
+                                         f"{1.0 - total_evals / total_sims:.3f}, budget 1 == callback")
+    assert total_evals < total_sims
+
+
+def test_more_than_65535_batches_per_thread(om):
+    """steps = ceil(S / L) has no upper limit (1 leaf per step, 70,000
+    simulations): the per-thread batch count must not run into the
+    waiting-for-NN flag. Every simulation reaches the root."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(45, 9, 128, 1, 32), device=0)
+    b = om.BatchedMCTS(2, history_size=4, num_simulations=70000, num_threads=1, batch_size=1,
+                       dirichlet_epsilon=0.0, seed=3, node_capacity=1 << 21)
+    sims, evals = b.search(net)
+    assert sims == 2 * 70000
+    for g in range(2):
+        info = b.root_info(g)
+        assert info["visit_count"] == 70000
+        assert sum(info["visit_counts"]) == 70000 - 1  # the first leaf is the unexpanded root
+    assert b.engine.status() == (0, 0)

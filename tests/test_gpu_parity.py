@@ -444,17 +444,18 @@ def test_gpu_async_search_matches_sync(om):
             acts.append(b.selfplay_move(temperature_moves=3, emit_targets=False)["actions"].clone())
         ms, launches, rows = b.engine.nn_timing()
         sel, bk, launches2 = b.engine.tree_timing()
-        steps = 64 // 32  # timed rounds (the 3 extra chain-splitting rounds carry no events)
-        assert launches2 == moves * steps * 2  # 2 pipeline groups at G >= 64
+        rounds = 64 // 32 + 3  # every round is timed, the 3 extra chain-splitting rounds included
+        assert launches2 == moves * rounds * 2  # 2 pipeline groups at G >= 64
         timed_groups = 2  # every group's NN launches carry events
-        assert launches == moves * steps * timed_groups
-        assert rows == moves * steps * (G // 2) * 32 * timed_groups
+        assert launches == moves * rounds * timed_groups
+        assert rows == moves * rounds * (G // 2) * 32 * timed_groups
         assert ms > 0 and sel > 0 and bk > 0
         # union of the launch intervals: at most their summed durations (two NN
         # chains by default, so the groups' launches may overlap)
         busy, tsims, tevals = b.engine.nn_busy()
         assert 0 < busy <= ms * 1.0001
-        assert 0 < tsims <= moves * G * 64 and 0 < tevals <= tsims  # timed rounds of every search
+        # every round of every (timed) search: all its simulations
+        assert tsims == moves * G * 64 and 0 < tevals <= tsims
         return torch.stack(acts).cpu().numpy(), [b.visit_counts(g) for g in range(G)]
 
     a_sync, v_sync = play(True)

@@ -56,6 +56,33 @@ def test_native_net_vs_reference_golden(om, golden_dir, name, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("name", ["c128b9_h8_r1027", "c128b9_h4_r1029", "c256b19_h8_r1025"])
+def test_throughput_geometry_vs_reference_golden(om, golden_dir, name, dtype):
+    """The geometries every bench launch runs (>= 1024 rows: 4-board C=128
+    workgroups with the LDS weight ring, 2-board C=256 workgroups with the
+    register-queue weight stream across all 39 convs) against the reference's
+    own AlphaZeroNet (neural_net.py:138-172) on >= 1025 real positions, ragged
+    in the last workgroup. The planes are regenerated from their seed
+    (ref_fixtures.real_features) and checked against the stored checksum."""
+    from ref_fixtures import planes_checksum, real_features
+
+    meta = json.loads((golden_dir / "resnet_large_meta.json").read_text())[name]
+    g = np.load(golden_dir / "resnet_large.npz")
+    x = real_features(meta["boards"], meta["history_size"], meta["planes_seed"])
+    assert planes_checksum(x) == meta["planes_sha256_16"]
+    assert len(x) >= 1024  # resnet.hip kSmallBatchRows: the throughput geometry
+    net = om.NativeNet(_sd(meta), device=0, dtype=dtype)
+    out = net(torch.from_numpy(x).to(DEV))
+    torch.cuda.synchronize()
+    dp = np.abs(out["policy"].cpu().numpy() - g[f"{name}_policy"]).max()
+    dv = np.abs(out["value"].cpu().numpy() - g[f"{name}_value"]).max()
+    numerics.record(f"resnet golden {name} {dtype} (throughput geometry)",
+                    f"max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e}")
+    tp, tv = TOL[dtype]
+    assert dp <= tp and dv <= tv
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("rows", [1, 3, 4, 5, 257, 1027, 2048])
 def test_native_net_vs_torch_fp32_restatement(om, rows, dtype):
     """Ragged batch sizes (partial last workgroup tile) on real-looking planes."""
@@ -236,12 +263,14 @@ def test_nn_batch_does_not_change_results(om):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
-@pytest.mark.parametrize("C,R", [(128, 9), (256, 3)])
+@pytest.mark.parametrize("C,R", [(128, 9), (256, 3), (256, 19)])
 def test_small_batch_geometry_is_bit_identical(om, dtype, C, R):
     """Fewer than 1024 rows run one board per workgroup (latency geometry);
     the K order per output is unchanged, so rows evaluated alone match the
     same rows inside a large (throughput-geometry) batch bit for bit. 1101
-    rows: the large batch's last workgroup is ragged (1101 = 4 x 275 + 1)."""
+    rows: the large batch's last workgroup is ragged (1101 = 4 x 275 + 1).
+    (256, 19) is configs[3]'s tower: the C=256 register queue runs on across
+    all 39 conv layers' boundaries into the zero pad."""
     from othello_mcts.synthetic import alphazero_state_dict
 
     net = om.NativeNet(alphazero_state_dict(11, 17, C, R, 64), device=0, dtype=dtype)

@@ -182,6 +182,25 @@ def test_resnet_restatement_matches_reference(golden_dir, name):
     np.testing.assert_allclose(out["value"].numpy(), g[f"{name}_value"], atol=2e-6, rtol=1e-4)
 
 
+@pytest.mark.parametrize("name", ["c128b9_h8_r1027", "c128b9_h4_r1029"])
+def test_resnet_restatement_matches_large_reference_goldens(golden_dir, name):
+    """The throughput-geometry goldens (>= 1024 rows, make_golden.py
+    make_resnet_large): the planes regenerate from their seed to the stored
+    checksum, and the fp32 restatement reproduces the reference's outputs (the
+    256x20b case is left to the GPU test: 3 TFLOP on the CPU)."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    meta = json.loads((golden_dir / "resnet_large_meta.json").read_text())[name]
+    g = np.load(golden_dir / "resnet_large.npz")
+    x = RF.real_features(meta["boards"], meta["history_size"], meta["planes_seed"])
+    assert RF.planes_checksum(x) == meta["planes_sha256_16"]
+    sd = alphazero_state_dict(meta["seed"], 1 + 2 * meta["history_size"], meta["conv_channels"],
+                              meta["num_residual_blocks"], meta["value_head_hidden_channels"])
+    out = resnet_ref.forward(sd, torch.from_numpy(x))
+    np.testing.assert_allclose(out["policy"].numpy(), g[f"{name}_policy"], atol=2e-6, rtol=1e-4)
+    np.testing.assert_allclose(out["value"].numpy(), g[f"{name}_value"], atol=2e-6, rtol=1e-4)
+
+
 # ---------------------------------------------------------------- reference-generated MCTS matrix
 import ref_fixtures as RF  # noqa: E402
 

@@ -7,6 +7,7 @@
 #   smoke                          __graft_entry__.smoke()           -> smoke.log
 #   bench NAME [bench.py args]     one bench line                    -> bench_NAME.json
 #   trace NAME [bench.py args]     rocprofv3 --kernel-trace --stats  -> trace_NAME/
+#   launch NAME [bench.py args]    bench.py --gpus 1 under torch.distributed.run (one RCCL rank)
 #   pmc NAME C1,C2,.. [bench args] one rocprofv3 --pmc pass (+ kernel trace) over bench.py -> pmc_NAME/
 #   nn NAME [VAR=val ...]          standalone k_resnet timing (tools/nn_kernel.py; ROWS, NN_C, NN_DTYPE)
 #   nnpmc NAME C1,C2,.. [VAR=val]  one --pmc pass over tools/nn_kernel.py  -> nnpmc_NAME/
@@ -43,6 +44,9 @@ run_recipe() {
     tests) step 600 "$OUT/tests.log" python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "$@" ;;
     smoke) step 300 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) local n=$1; shift; step 900 "$OUT/bench_$n.json" python bench.py "$@" ;;
+    launch) local n=$1; shift
+      step 900 "$OUT/launch_$n.json" python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 \
+        --master-addr=127.0.0.1 --master-port=29531 bench.py --gpus 1 "$@" ;;
     trace) local n=$1; shift
       step 600 "$OUT/trace_$n.log" rocprofv3 --kernel-trace --stats -T -d "$OUT/trace_$n" -o run \
         --output-format csv -- python3 bench.py "$@" ;;

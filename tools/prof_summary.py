@@ -42,23 +42,31 @@ def flops_per_row(C: int, R: int, in_ch: int = 17, hidden: int | None = None) ->
                  + 2 * 64 * hidden + 2 * hidden)
 
 
-def gather(dirs: list[str]):
-    """{counter: [per-dispatch values]} and [durations s] of the k_resnet dispatches."""
+def kernel_name_of(name: str) -> str:
+    """k_resnet_w8<...> / k_tree(...) -> k_resnet_w8 / k_tree."""
+    return re.split(r"[<(]", name.strip(), maxsplit=1)[0].split()[-1]
+
+
+def gather(dirs: list[str], kernel: str = "k_resnet", regular_only: bool = True):
+    """{counter: [per-dispatch values]} and [durations s] of the dispatches of
+    `kernel` (a kernel-name prefix)."""
     per = defaultdict(lambda: defaultdict(float))
     dur = {}
     for d in dirs:
         for f in glob.glob(f"{d}/**/run_counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
-                if "k_resnet" in r["Kernel_Name"]:
+                if kernel_name_of(r["Kernel_Name"]).startswith(kernel):
                     per[(d, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
         for f in glob.glob(f"{d}/**/run_kernel_trace.csv", recursive=True):
             for r in csv.DictReader(open(f)):
-                if "k_resnet" in r["Kernel_Name"]:
+                if kernel_name_of(r["Kernel_Name"]).startswith(kernel):
                     dur[(d, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-    # the chain-splitting extra rounds' launches evaluate only lagging games'
-    # rows (mostly none): bench.py leaves them out of its timing, and so does
-    # this summary (dispatches shorter than a quarter of the median)
-    if dur:
+    # per-launch counters of full launches: the chain-splitting extra rounds'
+    # launches evaluate only lagging games' rows (mostly none) and are left out
+    # of the per-launch averages (dispatches shorter than a quarter of the
+    # median); the bench line's roofline covers every launch (trace_summary
+    # cross-checks that)
+    if dur and regular_only:
         med = sorted(dur.values())[len(dur) // 2]
         keep = {k for k, v in dur.items() if v >= 0.25 * med}
         dur = {k: v for k, v in dur.items() if k in keep}
@@ -170,14 +178,33 @@ def bench_summary(outdir: str, prefix: str, tag: str) -> dict:
            "passes": [Path(d).name for d in dirs], "dispatches_timed": len(durs),
            "counters_per_launch": {k: round(v) for k, v in c.items()},
            "derived": derive(c, avg(durs), rows, fpr)}
+    # k_tree over the same passes (every round: select rounds, extra rounds and
+    # the final backups)
+    tby, tdurs = gather(dirs, "k_tree", regular_only=False)
+    tc = {k: avg(v) for k, v in sorted(tby.items())}
+    res["k_tree"] = {"dispatches_timed": len(tdurs), "counters_per_launch": {k: round(v) for k, v in tc.items()},
+                     "derived": derive(tc, avg(tdurs), None, None)}
     OUT.mkdir(exist_ok=True)
     (OUT / f"{tag}_bench_pmc.json").write_text(json.dumps(res, indent=1) + "\n")
+    sys.path.insert(0, str(ROOT))
+    from bench import kernel_hash  # noqa: E402  (the sources these passes ran)
+
     if "hbm_bytes_per_launch" in res["derived"] and bench:
         (OUT / "traffic_resnet.json").write_text(json.dumps({
             "tag": tag, "bytes_per_launch": res["derived"]["hbm_bytes_per_launch"],
             "workload": bench["config"]["workload"], "rows_per_launch": bench["roofline"]["rows_per_launch"],
+            "kernel_hash": kernel_hash("resnet"),
             "note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> B) per k_resnet launch, rocprofv3 --pmc, separate passes "
                     "(tools/prof_summary.py)"}, indent=1) + "\n")
+    td = res["k_tree"]["derived"]
+    if "hbm_bytes_per_launch" in td and bench:
+        (OUT / "traffic_tree.json").write_text(json.dumps({
+            "tag": tag, "kernels": {"k_tree": {"bytes_per_launch": td["hbm_bytes_per_launch"],
+                                               "avg_ms_rocprof": td.get("avg_launch_ms")}},
+            "workload": bench["config"]["workload"], "kernel_hash": kernel_hash("tree"),
+            "note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> B) per k_tree launch (every round of a search, final "
+                    "backups included), rocprofv3 --pmc, separate passes (tools/prof_summary.py)"},
+            indent=1) + "\n")
     return res
 
 
@@ -187,45 +214,79 @@ def trace_summary(outdir: str, name: str, tag: str) -> None:
     shutil.copy(stats, OUT / f"{tag}_kernel_stats.csv")
     trace = next(Path(outdir).glob(f"trace_{name}/**/run_kernel_trace.csv"), None)
     if trace is not None:
-        res = resnet_busy(trace)
+        res = resnet_busy(trace, bench_line(Path(outdir) / f"trace_{name}.log"))
         (OUT / f"{tag}_resnet_busy.json").write_text(json.dumps(res, indent=1) + "\n")
         print(json.dumps(res, indent=1))
 
 
-def resnet_busy(trace: Path) -> dict:
+def bench_line(log: Path) -> dict | None:
+    if not log.exists():
+        return None
+    for ln in log.read_text().splitlines():
+        if ln.startswith("{") and '"metric"' in ln:
+            return json.loads(ln)
+    return None
+
+
+def interval_union(xs) -> float:
+    """Length covered by [start, end] intervals (csrc/timing.h restated)."""
+    xs = sorted(xs)
+    busy, lo, hi = 0, None, None
+    for a, b in xs:
+        if hi is None or a > hi:
+            if hi is not None:
+                busy += hi - lo
+            lo, hi = a, b
+        else:
+            hi = max(hi, b)
+    return busy + (hi - lo if hi is not None else 0)
+
+
+def resnet_busy(trace: Path, bench: dict | None = None) -> dict:
     """k_resnet dispatches of a kernel trace: mean duration, and the union of
     their [start, end] intervals per dispatch (launches of different NN chains
-    overlap; bench.py's busy_ms_per_launch is the same union from HIP events)."""
+    overlap; bench.py's busy_ms_per_launch is the same union from HIP events).
+    With the bench line of the traced command: the roofline recomputed from the
+    trace alone — the timed region's rows (work.n_eval) x FLOPs per row over
+    the union of its dispatches (the last roofline.timed_region_launches
+    k_resnet dispatches: every round of every timed search) — next to the
+    line's own frac."""
     iv = []
     with open(trace) as f:
         for row in csv.DictReader(f):
-            if "k_resnet" in row["Kernel_Name"]:
+            if kernel_name_of(row["Kernel_Name"]).startswith("k_resnet"):
                 iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
-    def union(xs):
-        xs = sorted(xs)
-        busy, lo, hi = 0, None, None
-        for a, b in xs:
-            if hi is None or a > hi:
-                if hi is not None:
-                    busy += hi - lo
-                lo, hi = a, b
-            else:
-                hi = max(hi, b)
-        return busy + (hi - lo if hi is not None else 0)
-
+    iv.sort()
     n = max(1, len(iv))
     res = {"source": str(trace), "dispatches": len(iv),
            "avg_duration_ms": round(sum(b - a for a, b in iv) / n / 1e6, 4),
-           "busy_ms_per_dispatch": round(union(iv) / n / 1e6, 4)}
-    # without the chain-splitting extra rounds' near-empty launches (bench.py
-    # times only the regular rounds): dispatches >= a quarter of the median
-    if iv:
-        med = sorted(b - a for a, b in iv)[len(iv) // 2]
-        reg = [(a, b) for a, b in iv if b - a >= 0.25 * med]
-        m = max(1, len(reg))
-        res.update({"regular_dispatches": len(reg),
-                    "regular_avg_duration_ms": round(sum(b - a for a, b in reg) / m / 1e6, 4),
-                    "regular_busy_ms_per_dispatch": round(union(reg) / m / 1e6, 4)})
+           "busy_ms_per_dispatch": round(interval_union(iv) / n / 1e6, 4)}
+    if not bench:
+        return res
+    # the dispatches run in this order: warm-up, the timed region, then the
+    # `sustained` sub-record's moves (if any)
+    segs = [("timed_region", bench, bench.get("roofline", {}))]
+    if "sustained" in bench:
+        segs.append(("sustained", bench["sustained"], bench["sustained"]["roofline"]))
+    end = len(iv)
+    for name, rec, r in reversed(segs):
+        nt = r.get("timed_region_launches")
+        if not nt or end < nt:
+            break
+        tr = iv[end - nt:end]
+        end -= nt
+        busy_ms = interval_union(tr) / 1e6
+        n_eval = rec["work"]["n_eval"]
+        fpr = bench["roofline"]["flops_per_row"]
+        a = n_eval * fpr / (busy_ms * 1e-3) / 1e12
+        res[name] = {"dispatches": nt,
+                     "avg_duration_ms": round(sum(b - a_ for a_, b in tr) / nt / 1e6, 4),
+                     "busy_ms_per_dispatch": round(busy_ms / nt, 4),
+                     "n_eval": n_eval,
+                     "trace_achieved_TFLOP_s": round(a, 1), "trace_frac": round(a / r["peak"], 4),
+                     "bench_frac": r.get("frac"), "bench_busy_ms_per_launch": r.get("busy_ms_per_launch"),
+                     "bench_n_eval_per_launch": r.get("n_eval_per_launch"),
+                     "frac_rel_diff": round(r.get("frac", 0) / (a / r["peak"]) - 1, 4)}
     return res
 
 
