@@ -28,6 +28,14 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Orders this wave's earlier global stores before its later loads of the same
+// words, from any lane: the next descent / backup reads the statistics the
+// previous one stored. A wavefront-scope fence: the AMDGPU memory model needs
+// no wait for it on gfx950 (it emits none; a wave's vector memory operations
+// reach the cache in order), so the stores' write-back overlaps the next
+// descent's first loads instead of a vmcnt(0) drain per leaf.
+__device__ __forceinline__ void wave_order() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
 // Wave reductions with DPP (row_shr / row_bcast inclusive scan, the total ends
 // in lane 63): a few cycles per step, where __shfl_xor compiles to a chain of
 // ds_bpermute LDS round trips (the dominant cost of a k_select level).
@@ -159,6 +167,10 @@ __device__ __forceinline__ void write_packed_features(const EngineView& E, size_
                                                       bool valid) {
     const int lane = lane_id();
     uint64_t* row = E.feat + (size_t)r * E.FW;
+    if (!valid) {  // a terminal leaf: no NN row, only the meta word says so
+        if (lane == 0) row[0] = 0ULL;
+        return;
+    }
     // ancestor h = path[d - h] for h <= d, else hist[h - d - 1]
     const int idx = d - lane;
     const int from_p0 = __shfl(p0, idx & 63);
@@ -169,7 +181,7 @@ __device__ __forceinline__ void write_packed_features(const EngineView& E, size_
     if (idx >= 0) anc = idx < 64 ? from_p0 : from_p1;
     else if (hj < hist_n) anc = from_h;
     uint64_t a1 = 0, a2 = 0;
-    if (lane < E.H && anc >= 0 && valid) {
+    if (lane < E.H && anc >= 0) {
         const NodePos* np = E.pos + base + anc;
         a1 = np->p1;
         a2 = np->p2;
@@ -179,9 +191,7 @@ __device__ __forceinline__ void write_packed_features(const EngineView& E, size_
         row[3 + 2 * lane] = a2;
     }
     if (lane == 0) {
-        const uint64_t meta = valid ? ((uint64_t)((leaf_player - 1) & 1) | ((uint64_t)t << 8) |
-                                       (1ULL << 16))
-                                    : 0ULL;
+        const uint64_t meta = (uint64_t)((leaf_player - 1) & 1) | ((uint64_t)t << 8) | (1ULL << 16);
         row[0] = meta;
         row[1] = 0;
     }
@@ -326,7 +336,7 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
                 c0 = i + 1;
             }
         }
-        wait_stores();  // the next descent reads these statistics
+        wave_order();  // the next descent reads these statistics
     }
 }
 
@@ -447,7 +457,7 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
                     store_stat(E.stat + base + path1, s);
                 }
             }
-            wait_stores();  // the next leaf's backup reads these statistics
+            wave_order();  // the next leaf's backup reads these statistics
         }
     }
 }
