@@ -335,10 +335,10 @@ def parse_args(argv: list[str]):
     ap.add_argument("--round-robin-endgames", action="store_true",
                     help="all-terminal batches wait for their round instead of the reference's immediate "
                          "re-selection (oamd_engine_set_exact_interleaving(0)); default: exact")
-    ap.add_argument("--chain-budget", type=int, default=8,
+    ap.add_argument("--chain-budget", type=int, default=4,
                     help="re-selections after all-terminal batches per game and round before the chain is split "
                          "(0 = never split; exact interleaving only)")
-    ap.add_argument("--chain-cuts", type=int, default=3, help="chain splits per game and search (= extra rounds)")
+    ap.add_argument("--chain-cuts", type=int, default=8, help="chain splits per game and search (= extra rounds)")
     ap.add_argument("--cpu-baseline-moves", type=int, default=24,
                     help="timed moves of the CPU baseline (0 = skip it), after 2 warm-up moves")
     ap.add_argument("--cpu-baseline-threads", type=int, default=0,
@@ -464,14 +464,15 @@ class EngineWorkload:
 
     def stop_measuring(self) -> dict:
         e = self.b.engine
-        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), (bu0, ts0, te0) = self.t0
-        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), (bu1, ts1, te1) = (e.nn_timing(), e.tree_timing(),
-                                                                         e.work_counters(), e.nn_busy())
+        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), (bu0, bl0) = self.t0
+        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), (bu1, bl1) = (e.nn_timing(), e.tree_timing(),
+                                                                    e.work_counters(), e.nn_busy())
         overflow_games, depth_capped = e.status()
         if overflow_games or depth_capped:
             raise SystemExit(f"bench invalid: {overflow_games} game(s) overflowed their node pool, "
                              f"{depth_capped} hit the depth cap")
-        return {"nn_ms": ms1 - ms0, "nn_busy_ms": bu1 - bu0, "timed_evals": te1 - te0, "nn_launches": la1 - la0, "nn_rows": rw1 - rw0, "select_ms": se1 - se0,
+        return {"nn_ms": ms1 - ms0, "nn_busy_ms": bu1 - bu0, "busy_launches": bl1 - bl0, "nn_launches": la1 - la0,
+                "nn_rows": rw1 - rw0, "select_ms": se1 - se0,
                 "backup_ms": bk1 - bk0, "tree_launches": tl1 - tl0, "sims": si1 - si0, "evals": ev1 - ev0,
                 "overflow_games": overflow_games}
 
@@ -500,11 +501,9 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
     sustained = None
     if measuring and args.sustained_moves > 0:
         # the engine's real workload: the same games played on through their
-        # endgames (all-terminal batches, chain splitting) and restarts. Every
-        # search is timed: the work per search varies with the games' phase
-        # (the games start together, so their endgames coincide) and a
-        # 1-in-5 sample is biased (~1 % event cost)
-        wl.start_measuring(1)
+        # endgames (all-terminal batches, chain splitting) and restarts (the
+        # roofline covers every launch; HIP events sample every 5th search)
+        wl.start_measuring()
         dt_s = timed_max(world, lambda: steps(args.sustained_moves), wl.sync,
                          "cuda" if backend == "nccl" else "cpu")
         sustained = sustained_fields(args, wl.stop_measuring(), world, sims_per_search, dt_s)
@@ -612,11 +611,12 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     counters of this rank's timed region."""
     R = args.blocks - 1
     flops = resnet_flops_per_eval(1 + 2 * args.history, args.channels, R, args.hidden)
+    # the sampled searches' HIP-event span per launch (includes time a launch
+    # shared the CUs with the other NN chain's launch)
     avg_ms = m["nn_ms"] / max(1, m["nn_launches"])
-    # with --nn-chains > 1 the pipeline groups' launches overlap: each launch's
-    # event span then includes time it shared the CUs with another one, and the
-    # kernel's delivered rate is taken over the union of the launch intervals
-    busy_ms = m["nn_busy_ms"] / max(1, m["nn_launches"])
+    # busy: the union of the kernel-recorded execution intervals of EVERY
+    # ResNet launch in the window (oamd_engine_nn_busy), per launch
+    busy_ms = m["nn_busy_ms"] / max(1, m["busy_launches"])
     rows_per_launch = m["nn_rows"] / max(1, m["nn_launches"])
     # n_eval: rows of non-terminal leaves (BASELINE.md: the MFMA fraction is
     # over evaluated simulations); terminal rows are launched but their
@@ -624,11 +624,9 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     rows_launched = args.games * args.threads * args.batch * ((args.sims + args.threads * args.batch - 1)
                                                               // (args.threads * args.batch)) * args.steps
     eval_share = m["evals"] / max(1, rows_launched)
-    # the timed searches' own NN rows (device counters of every round of the
-    # timed searches, the chain-splitting extra rounds included), over those
-    # searches' launches, all rounds: rows, launches and busy time cover the
-    # same launches
-    n_eval_per_launch = m["timed_evals"] / max(1, m["nn_launches"])
+    # the window's NN rows (every search, every round), over the window's
+    # launches: rows, launches and busy time cover the same launches
+    n_eval_per_launch = m["evals"] / max(1, m["busy_launches"])
     achieved = flops * n_eval_per_launch / (busy_ms * 1e-3) / 1e12
     # every launched row counted as work (the round-2 basis): n_eval / eval_share
     achieved_launched = achieved / max(eval_share, 1e-9)
@@ -673,9 +671,10 @@ def measured_fields(args, m: dict, workload: str) -> dict:
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
-            "basis": ("n_eval rows (the timed searches' non-terminal leaves, every round) per launch x "
-                      "flops_per_row / busy ms per launch (the union of the timed searches' launch intervals, "
-                      "every round, / their launches; = avg_launch_ms when launches do not overlap)"),
+            "basis": ("n_eval rows (non-terminal leaves of every search and round in the timed region) per launch "
+                      "x flops_per_row / busy ms per launch (the union of the kernel-recorded execution intervals "
+                      "of every ResNet launch in the timed region / those launches)"),
+            "launches": m["busy_launches"],
             "timed_region_launches": timed_region_resnet_launches(args),
             "kernel_hash": kernel_hash("resnet"),
             "avg_launch_ms": round(avg_ms, 4),

@@ -200,6 +200,11 @@ int oamd_engine_set_exact_interleaving(oamd_engine *e, int32_t enable);
  * workgroup, 16 u64 per workgroup: see tools/nn_stamps.py) of the last launch. Only in builds
  * with OAMD_EXTRA_FLAGS=-DOAMD_STAMPS; otherwise OAMD_INVALID_ARGUMENT. */
 int oamd_debug_read_stamps(uint64_t *out, int64_t n);
+/* Diagnostics: k_tree's phase cycle sums over every wave since the last reset
+ * (tools/tree_stamps.py); reset != 0 zeroes them after the copy. Only in
+ * builds with OAMD_EXTRA_FLAGS=-DOAMD_TREE_STAMPS; otherwise
+ * OAMD_INVALID_ARGUMENT. */
+int oamd_debug_tree_stamps(uint64_t *out, int64_t n, int32_t reset);
 
 /* Step-wise search for an external evaluator (the Python NeuralNet callback
  * path, othello_mcts.cpp:36-45). Rows: row = game * L + leaf, L =
@@ -301,15 +306,16 @@ int oamd_engine_game_key(oamd_engine *e, int32_t game, uint64_t *key_host);
  * (terminal leaves included; oamd_engine_work_counters gives the rows that
  * needed an evaluation). */
 int oamd_engine_nn_timing(const oamd_engine *e, float *nn_ms, int64_t *launches, int64_t *rows);
-/* The union of those NN launch intervals (ms some timed ResNet launch was
- * running): equal to nn_ms when launches never overlap (one NN chain); with
- * oamd_engine_set_nn_chains(e, n > 1) the groups' launches overlap and nn_ms
- * counts the shared time once per launch. timed_sims / timed_evals: the
- * simulations and NN rows (non-terminal leaves) of those same timed searches
- * and rounds, so evals x FLOPs per row / busy is the delivered rate. Timed
- * are the rounds 1..ceil(S/L) of every timing_stride-th search; the extra
- * chain-splitting rounds (oamd_engine_set_chain_split) are not. */
-int oamd_engine_nn_busy(const oamd_engine *e, float *busy_ms, int64_t *timed_sims, int64_t *timed_evals);
+/* Busy time of the ResNet kernel: while timing is enabled, every ResNet
+ * launch of a native search (all searches, all rounds, the chain-splitting
+ * extra rounds included) records its execution interval in the kernel (first
+ * workgroup start to last workgroup end, s_memrealtime); busy_ms is the union
+ * of those intervals since timing was last enabled (ms some ResNet launch was
+ * running; launches of different NN chains and pipeline groups overlap),
+ * launches their count. The rows they evaluated are the difference of
+ * oamd_engine_work_counters over the same window, so evals x FLOPs per row /
+ * busy is the delivered rate. Waits for the device. */
+int oamd_engine_nn_busy(const oamd_engine *e, float *busy_ms, int64_t *launches);
 /* Same for the tree kernel (k_tree, one launch per search round and pipeline
  * group): select_ms = total ms of the rounds that select (each also backs up
  * the previous batch, thread by thread), backup_ms = total ms of the final
@@ -318,7 +324,9 @@ int oamd_engine_nn_busy(const oamd_engine *e, float *busy_ms, int64_t *timed_sim
  * record 4 HIP events per round and pipeline group on the group's stream. */
 int oamd_engine_tree_timing(const oamd_engine *e, float *select_ms, float *backup_ms, int64_t *launches);
 /* enable: 0 off, 1 time every search, N >= 2 time every N-th search (sampled:
- * a timed search's event packets lengthen the gaps between its launches). */
+ * a timed search's event packets lengthen the gaps between its launches).
+ * The ResNet busy-time window (oamd_engine_nn_busy) restarts here and covers
+ * every search while enable != 0; restarting waits for the device. */
 int oamd_engine_enable_timing(oamd_engine *e, int32_t enable);
 
 #ifdef __cplusplus

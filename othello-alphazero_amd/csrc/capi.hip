@@ -171,8 +171,8 @@ struct oamd_engine {
     // native search, exact interleaving: an all-terminal chain stops after
     // chain_budget re-selections in a round, at most chain_cuts times per
     // search (k_tree); chain_cuts extra rounds per search. 0 = never split
-    int chain_budget = 8;
-    int chain_cuts = 3;
+    int chain_budget = 4;
+    int chain_cuts = 8;
     int step_phase = 0;  // 1 = a selected round awaits its backup (step API)
     // pipeline groups (0 = auto) and their streams / fork-join events
     int pipeline = 0;
@@ -206,9 +206,20 @@ struct oamd_engine {
     int ev_nn_groups[2] = {1, 1};  // groups (0 .. n-1) whose NN launches carry events
     int64_t ev_launches[2] = {0, 0};  // k_resnet launches inside those blocks
     int64_t ev_rows[2] = {0, 0};
+    // NN busy time (oamd_engine_nn_busy): while timing is enabled, EVERY
+    // ResNet launch of a native search records its execution interval
+    // (kernel-side span, launch_resnet_packed: ~start, end in 100 MHz ticks)
+    // in a window of slots, zeroed when allocated and when the window
+    // restarts; the busy time is the union over the whole window (launches of
+    // the pipeline groups' searches overlap in time, and the groups drift
+    // apart over whole games, so per-search unions would count shared time
+    // twice). A search's slots are contiguous: [group][round][launch].
+    static constexpr int64_t kSpanChunk = 1 << 15;  // slots (2 x u64) per chunk
+    std::vector<unsigned long long*> span_chunks;
+    int64_t span_used = 0;      // slot index where the next search's block starts
+    int64_t span_launches = 0;  // slots handed out in the window
     int ev_cur = 0;
     float nn_ms = 0.0f;
-    float nn_busy_ms = 0.0f;  // union of the timed NN launch intervals
     float select_ms = 0.0f;
     float backup_ms = 0.0f;
     int64_t nn_launches = 0;
@@ -221,7 +232,6 @@ struct oamd_engine {
         // NN launch intervals relative to the search's first event: their
         // union is the time some ResNet launch ran (launches of different NN
         // chains overlap; with one chain the union is the sum of durations)
-        std::vector<std::pair<float, float>> iv;
         for (int i = 0; i < n; ++i) {
             const hipEvent_t* b = &ev[p][kEvPerBlock * i];
             float ms = 0.0f;
@@ -235,13 +245,9 @@ struct oamd_engine {
             if (nn) {
                 HIPCHK(hipEventElapsedTime(&ms, b[2], b[3]));
                 nn_ms += ms;
-                float t0 = 0.0f, t1 = 0.0f;
-                HIPCHK(hipEventElapsedTime(&t0, ev[p][0], b[2]));
-                HIPCHK(hipEventElapsedTime(&t1, ev[p][0], b[3]));
-                iv.emplace_back(t0, t1);
             }
         }
-        nn_busy_ms += (float)interval_union(iv);
+
         nn_launches += ev_launches[p];
         tree_launches += ev_final[p];
         nn_rows += ev_rows[p];
@@ -251,6 +257,36 @@ struct oamd_engine {
     int resolve_all_timing() {
         int rc = resolve_timing(ev_cur ^ 1);
         return rc ? rc : resolve_timing(ev_cur);
+    }
+    // n contiguous span slots for one search (nullptr when timing is off)
+    int reserve_spans(int64_t n, unsigned long long** out) {
+        *out = nullptr;
+        if (!timing || n <= 0 || n > kSpanChunk) return OAMD_OK;
+        int64_t c = span_used / kSpanChunk, off = span_used % kSpanChunk;
+        if (off + n > kSpanChunk) {
+            ++c;
+            off = 0;
+        }
+        while ((int64_t)span_chunks.size() <= c) {
+            unsigned long long* x = nullptr;
+            if (int rc = dalloc(&x, (size_t)2 * kSpanChunk)) return rc;
+            HIPCHK(hipMemset(x, 0, sizeof(unsigned long long) * 2 * kSpanChunk));
+            span_chunks.push_back(x);
+        }
+        *out = span_chunks[c] + 2 * off;
+        span_used = c * kSpanChunk + off + n;
+        span_launches += n;
+        return OAMD_OK;
+    }
+    // restart the window: every launch that may still write a slot is done
+    int reset_spans() {
+        if (!span_used) return OAMD_OK;
+        HIPCHK(hipDeviceSynchronize());
+        for (int64_t c = 0; c * kSpanChunk < span_used; ++c)
+            HIPCHK(hipMemset(span_chunks[c], 0, sizeof(unsigned long long) * 2 * kSpanChunk));
+        span_used = 0;
+        span_launches = 0;
+        return OAMD_OK;
     }
 
     int L() const { return cfg.num_threads * cfg.batch_size; }
@@ -381,6 +417,7 @@ struct oamd_engine {
         dfree(spd_dev);
         for (auto& pool : ev)
             for (auto e : pool) (void)hipEventDestroy(e);
+        for (auto& x : span_chunks) dfree(x);
         for (int k = 0; k < n_pipe_streams; ++k) {
             (void)hipStreamDestroy(pipe_stream[k]);
             (void)hipEventDestroy(join_ev[k]);
@@ -874,6 +911,8 @@ int oamd_engine_backup(oamd_engine* e) {
 
 int oamd_engine_enable_timing(oamd_engine* e, int32_t enable) {
     if (enable < 0) return fail(OAMD_INVALID_ARGUMENT, "enable_timing: expected >= 0");
+    DeviceGuard dg(e->device);
+    if (int rc = e->reset_spans()) return rc;
     e->timing = enable != 0;
     e->timing_stride = enable > 1 ? enable : 1;
     e->search_count = 0;
@@ -889,17 +928,26 @@ int oamd_engine_nn_timing(const oamd_engine* ce, float* nn_ms, int64_t* launches
     return OAMD_OK;
 }
 
-int oamd_engine_nn_busy(const oamd_engine* ce, float* busy_ms, int64_t* timed_sims, int64_t* timed_evals) {
+int oamd_engine_nn_busy(const oamd_engine* ce, float* busy_ms, int64_t* launches) {
     oamd_engine* e = const_cast<oamd_engine*>(ce);
-    if (int rc = e->resolve_all_timing()) return rc;
-    if (busy_ms) *busy_ms = e->nn_busy_ms;
-    if (timed_sims || timed_evals) {
-        DeviceGuard dg(e->device);
-        unsigned long long c[2] = {0, 0};
-        HIPCHK(hipMemcpy(c, e->counters + 4, sizeof(c), hipMemcpyDeviceToHost));
-        if (timed_sims) *timed_sims = (int64_t)c[0];
-        if (timed_evals) *timed_evals = (int64_t)c[1];
+    DeviceGuard dg(e->device);
+    std::vector<std::pair<float, float>> iv;
+    if (e->span_used) {
+        HIPCHK(hipDeviceSynchronize());  // every launch of the window has written its slot
+        std::vector<unsigned long long> sp((size_t)2 * e->span_used);
+        for (int64_t c = 0; c * oamd_engine::kSpanChunk < e->span_used; ++c) {
+            const int64_t n = std::min(oamd_engine::kSpanChunk, e->span_used - c * oamd_engine::kSpanChunk);
+            HIPCHK(hipMemcpy(sp.data() + 2 * c * oamd_engine::kSpanChunk, e->span_chunks[c],
+                             sizeof(unsigned long long) * 2 * n, hipMemcpyDeviceToHost));
+        }
+        unsigned long long t0 = ~0ULL;
+        for (int64_t i = 0; i < e->span_used; ++i)
+            if (sp[2 * i + 1]) t0 = std::min(t0, ~sp[2 * i]);
+        for (int64_t i = 0; i < e->span_used; ++i)  // 100 MHz ticks -> ms, from the window's first start
+            if (sp[2 * i + 1]) iv.emplace_back((float)((~sp[2 * i] - t0) * 1e-5), (float)((sp[2 * i + 1] - t0) * 1e-5));
     }
+    if (busy_ms) *busy_ms = (float)interval_union(iv);
+    if (launches) *launches = e->span_launches;
     return OAMD_OK;
 }
 
@@ -954,6 +1002,17 @@ static int extra_rounds(const oamd_engine* e) {
 // a thread plus the chain-splitting extra rounds
 static int search_rounds(const oamd_engine* e, int steps) { return steps + extra_rounds(e); }
 
+// ResNet launches per group and round (the most of any group: nn_batch splits
+// a group's rows into consecutive launches)
+static int launches_per_group_round(const oamd_engine* e, const GroupPlan& P) {
+    int n = 1;
+    for (int k = 0; k < P.K; ++k) {
+        const int grows = P.ng[k] * e->L(), cb = e->nn_batch > 0 ? e->nn_batch : grows;
+        n = std::max(n, (grows + cb - 1) / cb);
+    }
+    return n;
+}
+
 // Sampled timing of one search: claim the current event pool (every
 // timing_stride-th search), sized for NB blocks per round and `steps` NN
 // rounds (search_rounds) plus the final backup-only round.
@@ -962,6 +1021,7 @@ static int timing_begin(oamd_engine* e, int steps, int NB, bool* timed) {
     if (!*timed) return OAMD_OK;
     const int pool = e->ev_cur;
     if (int rc = e->resolve_timing(pool)) return rc;
+
     while ((int)e->ev[pool].size() < kEvPerBlock * (steps + 1) * NB) {
         hipEvent_t x;
         HIPCHK(hipEventCreate(&x));
@@ -1014,6 +1074,9 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
     // records events for every round, the extra ones included, and counts the
     // NN rows of every round (counters [4..5]): launches, rows and busy time
     // of a timed search cover the same launches (search_rounds)
+    const int nlg = launches_per_group_round(e, P);
+    unsigned long long* span = nullptr;  // this search's busy-time slots (timing on)
+    if (int rc = e->reserve_spans((int64_t)K * S * nlg, &span)) return rc;
     for (int s = 0; s <= S; ++s) {
         for (int k = 0; k < K; ++k) {
             const size_t r0 = (size_t)P.g0[k] * L;
@@ -1040,9 +1103,10 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
             if (ev) HIPCHK(hipEventRecord(ev[2], ns));
             const int grows = P.ng[k] * L;
             const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
-            for (int r = 0; r < grows; r += cb)
+            for (int r = 0, j = 0; r < grows; r += cb, ++j)
                 launch_resnet_packed(N, E.feat, E.FW, E.H, std::min(cb, grows - r), E.policy, E.value, ns,
-                                     E.rowlist + r0 + r, cnt + (s & 1), r);
+                                     E.rowlist + r0 + r, cnt + (s & 1), r,
+                                     span ? span + (size_t)2 * ((k * S + s) * nlg + j) : nullptr);
             if (ev) HIPCHK(hipEventRecord(ev[3], ns));
             if (K > 1 && OAMD_NN_ORDER == 2) {
                 HIPCHK(hipEventRecord(e->nn_ev[k], ns));
@@ -1102,6 +1166,8 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     const int rounds = split ? steps : search_rounds(e, steps);  // NN rounds
     if ((rc = timing_begin(e, rounds, NB, &timed))) return rc;
     const int pool = e->ev_cur;
+    unsigned long long* span = nullptr;  // busy-time slots [thread][round] of the split schedule
+    if (split && (rc = e->reserve_spans((int64_t)T * steps, &span))) return rc;
     for (int s = 0; split && s <= steps; ++s) {
         for (int t = 0; t < T; ++t) {
             hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * T + t)] : nullptr;
@@ -1115,7 +1181,8 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
             HIPCHK(hipStreamWaitEvent(ns, e->sel_ev[t], 0));
             if (ev) HIPCHK(hipEventRecord(ev[2], ns));
             launch_resnet_packed(N, E.feat + (size_t)t * B * E.FW, E.FW, E.H, B, E.policy + (size_t)t * B * 65,
-                                 E.value + (size_t)t * B, ns);
+                                 E.value + (size_t)t * B, ns, nullptr, nullptr, 0,
+                                 span ? span + (size_t)2 * (t * steps + s) : nullptr);
             if (ev) HIPCHK(hipEventRecord(ev[3], ns));
             HIPCHK(hipEventRecord(e->nn_ev[t], ns));
         }
@@ -1162,6 +1229,13 @@ int oamd_debug_read_stamps(uint64_t* out, int64_t n) {
     const int rc = resnet_read_stamps(reinterpret_cast<unsigned long long*>(out), (long long)n);
     if (rc == -2) return fail(OAMD_INVALID_ARGUMENT, "built without OAMD_STAMPS");
     return rc ? fail(OAMD_RUNTIME, "stamp copy failed") : OAMD_OK;
+}
+
+int oamd_debug_tree_stamps(uint64_t* out, int64_t n, int32_t reset) {
+    if (!out || n < 0) return fail(OAMD_INVALID_ARGUMENT, "tree stamps: bad buffer");
+    const int rc = tree_read_stamps(reinterpret_cast<unsigned long long*>(out), (long long)n, reset);
+    if (rc == -2) return fail(OAMD_INVALID_ARGUMENT, "built without OAMD_TREE_STAMPS");
+    return rc ? fail(OAMD_RUNTIME, "tree stamp copy failed") : OAMD_OK;
 }
 
 int oamd_engine_set_nn_chains(oamd_engine* e, int32_t chains) {

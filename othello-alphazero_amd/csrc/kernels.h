@@ -67,9 +67,13 @@ struct NetView {
 // Packed rows with an evaluation list (rowlist != nullptr): the launch
 // evaluates rows rowlist[0 .. min(rows, *rowcount - list_off)) (absolute row
 // indices into feat / policy / value); without one, rows 0 .. rows-1.
+// span != nullptr (timed searches): the launch records its execution interval
+// in span[0] = ~(earliest workgroup start), span[1] = latest workgroup end
+// (s_memrealtime, 100 MHz ticks; zero-initialised by the caller)
 void launch_resnet_packed(const NetView& N, const uint64_t* feat, int fw, int H, int rows,
                           float* policy, float* value, hipStream_t s, const int32_t* rowlist = nullptr,
-                          const int32_t* rowcount = nullptr, int list_off = 0);
+                          const int32_t* rowcount = nullptr, int list_off = 0,
+                          unsigned long long* span = nullptr);
 void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* policy, float* value,
                        hipStream_t s);
 size_t resnet_packed_weight_elems(int C, int R);
@@ -79,6 +83,7 @@ size_t resnet_head_floats(int C, int hidden);
 inline size_t resnet_hconv_elems(int C) { return (size_t)(C / 32) * 64 * 8; }
 // diagnostic stamp buffer (OAMD_STAMPS builds; -2 otherwise), see resnet.hip
 int resnet_read_stamps(unsigned long long* out, long long n);
+int tree_read_stamps(unsigned long long* out, long long n, int reset);
 // Weight K-step schedule shared by the kernel and the host packer: a K-step is
 // one 3x3 tap x 32 input channels. K-steps per conv (first conv: input zero-
 // padded to 32 channels, 9 K-steps rounded up to whole weight stages with

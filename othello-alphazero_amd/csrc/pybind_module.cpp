@@ -678,9 +678,9 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
         })
         .def("nn_busy", [](Engine& e) {
             float ms = 0.0f;
-            int64_t sims = 0, evals = 0;
-            check(oamd_engine_nn_busy(e.h, &ms, &sims, &evals));
-            return py::make_tuple(ms, sims, evals);
+            int64_t launches = 0;
+            check(oamd_engine_nn_busy(e.h, &ms, &launches));
+            return py::make_tuple(ms, launches);
         })
         .def("work_counters", [](Engine& e) {
             int64_t sims = 0, evals = 0;

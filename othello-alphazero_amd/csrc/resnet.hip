@@ -358,6 +358,7 @@ struct RowMap {
     const int32_t* count;  // filled entries + off (list entries before this launch)
     int off;
     int rows;
+    unsigned long long* span;  // launch interval (launch_resnet_packed), or nullptr
 };
 // row of launch entry r (= workgroup row0 + board), -1 past the end
 __device__ __forceinline__ int map_row(const RowMap& M, int r) {
@@ -1200,7 +1201,17 @@ template <class G, int DT, int IN>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_num_vgpr(OAMD_VGPR_CAP))) void k_resnet_w8(
     NetView N, const void* __restrict__ feat_in, int fw, int H, RowMap M, float* __restrict__ policy,
     float* __restrict__ value) {
+    // timed searches: the launch's execution interval over all its workgroups
+    // (the union of these intervals is the bench's busy time; a HIP event pair
+    // would add the dispatch latency of every launch, which near-empty
+    // endgame launches nobody overlaps make visible). Every early return of
+    // resnet_body is workgroup-uniform, so all threads meet at the barrier.
+    if (M.span && threadIdx.x == 0) atomicMax(M.span, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
     resnet_body<G, DT, IN>(N, feat_in, fw, H, M, policy, value);
+    if (M.span) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(M.span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
 }
 
 template <class G, int DT, int IN>
@@ -1253,13 +1264,13 @@ static void dispatch(const NetView& N, const void* feat, int fw, int H, const Ro
 
 void launch_resnet_packed(const NetView& N, const uint64_t* feat, int fw, int H, int rows,
                           float* policy, float* value, hipStream_t s, const int32_t* rowlist,
-                          const int32_t* rowcount, int list_off) {
-    dispatch<kPacked>(N, feat, fw, H, RowMap{rowlist, rowcount, list_off, rows}, policy, value, s);
+                          const int32_t* rowcount, int list_off, unsigned long long* span) {
+    dispatch<kPacked>(N, feat, fw, H, RowMap{rowlist, rowcount, list_off, rows, span}, policy, value, s);
 }
 
 void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* policy, float* value,
                        hipStream_t s) {
-    dispatch<kF32>(N, feat, 0, 0, RowMap{nullptr, nullptr, 0, rows}, policy, value, s);
+    dispatch<kF32>(N, feat, 0, 0, RowMap{nullptr, nullptr, 0, rows, nullptr}, policy, value, s);
 }
 
 int resnet_read_stamps(unsigned long long* out, long long n) {

@@ -26,6 +26,27 @@ namespace oamd {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+#ifndef OAMD_CHAIN_PRIO
+#define OAMD_CHAIN_PRIO 2
+#endif
+
+// Diagnostic build only (-DOAMD_TREE_STAMPS, tools/tree_stamps.py): cycle
+// sums of k_tree's phases (s_memtime), per wave in LDS (k_tree blocks are one
+// wave), added to g_tree_stamps when the wave ends. Nothing else reads them.
+#ifdef OAMD_TREE_STAMPS
+enum TreeStamp {
+    kTsWaves, kTsCycles, kTsDescent, kTsLevels, kTsLeaves, kTsPost, kTsBackup, kTsBackedUp, kTsTerminal,
+    kTsMaxCycles, kTsBatches, kTsSelect, kTsCount
+};
+__device__ unsigned long long g_tree_stamps[kTsCount];
+__shared__ unsigned long long ts_acc[kTsCount];
+#define TS_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define TS_ADD(i, x) do { if (lane_id() == 0) ts_acc[i] += (unsigned long long)(x); } while (0)
+#else
+#define TS_T(v) ((void)0)
+#define TS_ADD(i, x) ((void)0)
+#endif
+
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Orders this wave's earlier global stores before its later loads of the same
@@ -243,6 +264,7 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
         // exploration rate of `node` (from its N); for a chosen child it was
         // fetched by the child's lane at the previous level
         float er = explore_rate(E, root_n);
+        TS_T(ts0);
         // One dependent memory round trip per level: the stats AND links of all
         // children are loaded together; the chosen child's link, N and
         // exploration rate come from its lane (readlane), not from a second load.
@@ -291,6 +313,11 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
             lk = NodeLink{clk4.x, clk4.y, clk4.z, clk4.w};
             er = er_next;
         }
+        TS_T(ts1);
+        TS_ADD(kTsDescent, ts1 - ts0);
+        TS_ADD(kTsLevels, d);
+        TS_ADD(kTsLeaves, 1);
+        TS_ADD(kTsTerminal, lk.player == 0 ? 1 : 0);
         if (d == kMaxDepth - 1 && lk.player != 0 && lk.n_children != 0 && lane == 0)
             atomicOr(&gs->flags, (int)kDepthCap);
         // virtual loss on the path excluding the root (search_thread.cpp:69-76)
@@ -337,6 +364,8 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
             }
         }
         wave_order();  // the next descent reads these statistics
+        TS_T(ts2);
+        TS_ADD(kTsPost, ts2 - ts1);
     }
 }
 
@@ -346,6 +375,8 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
 __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t base, int i0, int i1,
                                              int& count, bool& overflow) {
     const int lane = lane_id();
+    TS_T(tb0);
+    TS_ADD(kTsBackedUp, i1 - i0);
     // Leaves are processed in order (their backups share path nodes), but
     // everything a leaf needs except the path statistics is independent of
     // the earlier leaves: it is fetched for up to 64 leaves at once, one lane
@@ -460,6 +491,8 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
             wave_order();  // the next leaf's backup reads these statistics
         }
     }
+    TS_T(tb1);
+    TS_ADD(kTsBackup, tb1 - tb0);
 }
 
 // ---------------------------------------------------------------------------
@@ -503,6 +536,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
+#ifdef OAMD_TREE_STAMPS
+    if (lane < kTsCount) ts_acc[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    TS_T(tk0);
+#endif
     GameState* gs = E.games + g;
     const size_t base = (size_t)g * E.cap;
     const int flags = gs->flags;
@@ -559,8 +597,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
                 break;
             }
             const unsigned long long ev0 = evals;
+            TS_T(tsel0);
             select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals, cnt_add,
                          g0 * E.L);
+            TS_T(tsel1);
+            TS_ADD(kTsSelect, tsel1 - tsel0);
+            TS_ADD(kTsBatches, 1);
             ++sel;
             if (evals != ev0 || !E.terminal_skip) {
                 pend = true;
@@ -568,6 +610,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
                 backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
                 again = true;
                 ++chain;
+#if OAMD_CHAIN_PRIO > 0
+                // an all-terminal chain holds its pipeline group's round (and so
+                // its NN launch): from its first re-selection on, this wave
+                // issues ahead of the other group's ResNet waves (priority 1)
+                if (chain == 1) __builtin_amdgcn_s_setprio(OAMD_CHAIN_PRIO);
+#endif
             }
         }
         if (lane == 0) *ts = sel | (pend ? kTstatePend : 0);
@@ -582,6 +630,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
         // atomic like select_range's kDepthCap: a plain read-modify-write of
         // the flags read at kernel start could drop that bit
         if (overflow) atomicOr(&gs->flags, (int)kOverflow);
+#ifdef OAMD_TREE_STAMPS
+        {
+            TS_T(tk1);
+            ts_acc[kTsWaves] = 1;
+            ts_acc[kTsCycles] = tk1 - tk0;
+            for (int i = 0; i < kTsCount; ++i) {
+                if (i == kTsMaxCycles) atomicMax(&g_tree_stamps[i], tk1 - tk0);
+                else atomicAdd(&g_tree_stamps[i], ts_acc[i]);
+            }
+        }
+#endif
         if (E.counters && do_select) {
             // [0..1] this search (reset when a caller asks for them), [2..3]
             // cumulative since the engine was created (oamd_engine_work_counters)
@@ -1053,4 +1112,26 @@ void launch_apply_positions(const Pos* in, const int32_t* actions, Pos* out, int
     if (n > 0) hipLaunchKernelGGL(k_apply_positions, dim3(blocks_for(n, 256)), dim3(256), 0, s, in, actions, out, n);
 }
 
+}  // namespace oamd
+
+namespace oamd {
+int tree_read_stamps(unsigned long long* out, long long n, int reset) {
+#ifdef OAMD_TREE_STAMPS
+    if (n > kTsCount) n = kTsCount;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tree_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[kTsCount] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tree_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+            return -1;
+    }
+    return 0;
+#else
+    (void)out;
+    (void)n;
+    (void)reset;
+    return -2;
+#endif
+}
 }  // namespace oamd

@@ -15,11 +15,13 @@ sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 
 
-def _m(launches=56, busy_per=0.75, span_per=1.05, rows=4096, evals_share=0.9, steps=10):
-    # one timed search, 2 pipeline groups x 28 rounds (25 + 3 chain-splitting extra rounds)
-    return {"nn_ms": span_per * launches, "nn_busy_ms": busy_per * launches, "nn_launches": launches,
-            "nn_rows": rows * launches, "timed_evals": int(rows * evals_share * launches),
-            "select_ms": 0.45 * 28 * 2, "backup_ms": 0.13 * 2, "tree_launches": 28 * 2,
+def _m(launches=66, busy_per=0.75, span_per=1.05, rows=4096, evals_share=0.9, steps=10):
+    # one sampled (HIP-event) search: 2 pipeline groups x 33 rounds (25 + 8
+    # chain-splitting extra rounds); busy time and rows over every launch of
+    # the window (steps searches)
+    return {"nn_ms": span_per * launches, "nn_busy_ms": busy_per * launches * steps, "nn_launches": launches,
+            "busy_launches": launches * steps, "nn_rows": rows * launches,
+            "select_ms": 0.45 * 33 * 2, "backup_ms": 0.13 * 2, "tree_launches": 33 * 2,
             "sims": 256 * 800 * steps, "evals": int(256 * 800 * steps * evals_share), "overflow_games": 0}
 
 
@@ -29,7 +31,7 @@ def test_roofline_uses_union_busy_time_and_timed_rows():
     out = bench.measured_fields(args, m, "w")
     r = out["roofline"]
     flops = bench.resnet_flops_per_eval(17, 128, 9, 128)
-    n_eval = m["timed_evals"] / m["nn_launches"]
+    n_eval = m["evals"] / m["busy_launches"]
     expect = flops * n_eval / (0.75e-3) / 1e12
     assert r["achieved"] == pytest.approx(expect, rel=1e-4)
     assert r["frac"] == pytest.approx(expect / 2500.0, abs=1e-4)
@@ -38,7 +40,7 @@ def test_roofline_uses_union_busy_time_and_timed_rows():
     share = out["work"]["n_eval"] / out["work"]["rows_launched"]
     assert r["achieved_rows_launched"] == pytest.approx(r["achieved"] / share, rel=1e-3)
     assert out["work"]["terminal_share"] == pytest.approx(0.1, abs=1e-3)
-    # tree: 28 select rounds per search and group (3 extra), one final backup each
+    # tree: 33 select rounds per search and group (8 extra), one final backup each
     t = out["tree_kernels"]
     assert t["k_tree"]["avg_launch_ms"] == pytest.approx(0.45)
     assert t["k_tree_final_backup"]["avg_launch_ms"] == pytest.approx(0.13)
@@ -55,18 +57,18 @@ def test_rounds_and_timed_region_launches():
     chain-splitting extra rounds (exact interleaving only); the timed region's
     k_resnet dispatches are steps x groups x rounds x launches per group."""
     a = bench.parse_args([])
-    assert bench.search_rounds(a) == 28 and bench.pipeline_groups(a) == 2
-    assert bench.timed_region_resnet_launches(a) == 10 * 2 * 28
+    assert bench.search_rounds(a) == 33 and bench.pipeline_groups(a) == 2
+    assert bench.timed_region_resnet_launches(a) == 10 * 2 * 33
     a = bench.parse_args(["--round-robin-endgames"])
     assert bench.search_rounds(a) == 25
     a = bench.parse_args(["--chain-budget", "0", "--steps", "4"])
     assert bench.timed_region_resnet_launches(a) == 4 * 2 * 25
     # configs[4] shard: 2048-row launches over 512 games (2 x 8192-row groups)
     a = bench.parse_args(["--games", "512", "--dtype", "fp16", "--eval-batch", "2048", "--steps", "3"])
-    assert bench.timed_region_resnet_launches(a) == 3 * 28 * 2 * 4
+    assert bench.timed_region_resnet_launches(a) == 3 * 33 * 2 * 4
     # configs[3]: 1600 sims = 50 batches per thread
     a = bench.parse_args(["--sims", "1600", "--channels", "256", "--blocks", "20"])
-    assert bench.search_rounds(a) == 53
+    assert bench.search_rounds(a) == 58
     # one game, T > 1: the thread-split schedule has no extra rounds
     a = bench.parse_args(["--games", "1"])
     assert bench.single_game_split(a) and bench.search_rounds(a) == 25
@@ -78,19 +80,16 @@ def test_n_eval_per_launch_within_launched_rows_with_extra_rounds():
     rows per launch still cover every launch of the timed searches: n_eval per
     launch <= rows per launch x (1 - terminal share)."""
     args = bench.parse_args(["--steps", "10"])
-    # 2 timed searches: 2 x 2 x 28 launches of 4096-row capacity; the regular
+    # 10 searches: 10 x 2 x 33 launches of 4096-row capacity; the regular
     # rounds hold 0.9 of the rows as non-terminal, the extra rounds 2 %
-    launches = 2 * 2 * 28
-    timed = int(2 * 2 * (25 * 4096 * 0.9 + 3 * 4096 * 0.02))
-    m = _m(launches=launches)
-    m["timed_evals"] = timed
-    m["evals"] = int(timed * 5)  # every 5th search timed
+    m = _m(launches=2 * 33)
+    m["evals"] = int(10 * 2 * (25 * 4096 * 0.9 + 8 * 4096 * 0.02))
     m["sims"] = 256 * 800 * 10
     out = bench.measured_fields(args, m, "w")
     r = out["roofline"]
     share = out["work"]["terminal_share"]
     assert r["n_eval_per_launch"] <= r["rows_per_launch"] * (1 - share) + 1e-6
-    assert r["timed_region_launches"] == 10 * 2 * 28
+    assert r["timed_region_launches"] == 10 * 2 * 33
     assert len(r["kernel_hash"]) == 16
 
 
@@ -158,4 +157,4 @@ def test_sustained_record_uses_its_own_moves():
     assert out["moves"] == 64 and out["value"] == pytest.approx(256 * 800 * 64 / 2.56, rel=1e-6)
     assert out["work"]["rows_launched"] == 256 * 800 * 64
     assert out["work"]["terminal_share"] == pytest.approx(0.15, abs=1e-3)
-    assert out["roofline"]["timed_region_launches"] == 64 * 2 * 28
+    assert out["roofline"]["timed_region_launches"] == 64 * 2 * 33

@@ -17,6 +17,7 @@
 #                                  for bit with the first variant's
 #   stamps NAME VARIANT [VAR=val]  tools/nn_stamps.py with abv/VARIANT (built with -DOAMD_STAMPS)
 #   benchvar NAME [bench args]     bench line of every prebuilt variant, ROUNDS interleaved sweeps
+#   treestamps NAME [VAR=val]      tools/tree_stamps.py with abv/ts (tools/tree_stamps_build.sh)
 # Trace post-processing: tools/kt_gaps.py (gaps between ResNet launches), tools/round_profile.py
 # (a step split by round). Every step runs under its own time limit; the first failing step ends the run
 # (no retries). Summaries: python tools/prof_summary.py (in the build container).
@@ -72,6 +73,11 @@ run_recipe() {
       cp $PKG/liboamd.so /tmp/liboamd.so.orig
       cp abv/$v/liboamd.so $PKG/liboamd.so
       step 300 "$OUT/stamps_$n.log" env "$@" python tools/nn_stamps.py; local rc=$?
+      restore_lib; return $rc ;;
+    treestamps) local n=$1; shift
+      cp $PKG/liboamd.so /tmp/liboamd.so.orig
+      cp abv/ts/liboamd.so $PKG/liboamd.so
+      step 600 "$OUT/treestamps_$n.log" env "$@" python -u tools/tree_stamps.py; local rc=$?
       restore_lib; return $rc ;;
     benchvar) local n=$1; shift
       cp $PKG/liboamd.so /tmp/liboamd.so.orig

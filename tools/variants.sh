@@ -2,7 +2,8 @@
 # Build liboamd.so variants HERE (CPU container) for the GPU-box recipes
 # `variants` / `benchvar` of tools/gpu.sh:
 #   VARIANTS="name:extra flags[:SRC];name2:..." bash tools/variants.sh
-# SRC: empty = the tree's resnet.hip with the tree's tree/capi objects;
+# SRC: empty = the tree's resnet.hip with the tree's tree/capi objects; + =
+# every unit of the working tree built with the flags;
 # a path = that resnet.hip with the tree's tree/capi objects; @REV = all of
 # csrc/ and include/ at git revision REV (capi.hip packs the weights, so a
 # variant that changes the packing must bring its own capi). Built into
@@ -22,7 +23,12 @@ for e in "${SETS[@]}"; do
   mkdir -p abv/$name
   (
     set -e
-    if [[ "${src:-}" == @* ]]; then
+    if [[ "${src:-}" == "+" ]]; then  # every unit of the working tree, built with the flags
+      $CXX -I $CS -I include $flags $RF -c $CS/resnet.hip -o abv/$name/resnet.o
+      $CXX -I $CS -I include $flags $EXACT -c $CS/tree.hip -o abv/$name/tree.o
+      $CXX -I $CS -I include $flags $EXACT -c $CS/capi.hip -o abv/$name/capi.o
+      objs="abv/$name/tree.o abv/$name/capi.o"
+    elif [[ "${src:-}" == @* ]]; then
       rev=${src#@}; d=abv/$name/src; mkdir -p $d
       git archive "$rev" othello-alphazero_amd/csrc include | tar -x -C $d
       inc="-I $d/$CS -I $d/include"
