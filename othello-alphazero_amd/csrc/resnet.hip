@@ -55,6 +55,11 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 constexpr int kLdsBytes = 160 * 1024;
 #ifdef OAMD_STAMPS
 constexpr int kMaxStampWgs = 1 << 16;
+// u64 per workgroup: 0-15 wave 0's stamps (tools/nn_stamps.py), 16-22 cycle
+// sums over all 8 waves: step-start lgkmcnt waits, stage-open vmcnt waits,
+// stage barriers, epilogue first barrier / stores / second barrier + reads,
+// tower cycles
+constexpr int kStampStride = 24;
 #endif
 // Weight stream: 16 KiB stages (2 K-steps at C=128, 1 at C=256) in a 3-slot
 // LDS ring (the small-batch geometry: 4 slots), refilled by LDS-DMA. 8 KiB
@@ -488,18 +493,18 @@ __host__ __device__ constexpr int head_scratch_floats(int hidden) {
 // records s_memrealtime (100 MHz) at kernel entry, after the prologue barrier,
 // after the tower, and at exit, plus s_memtime cycles across the tower and the
 // hardware id of its CU. Nothing else reads this buffer.
-__device__ unsigned long long g_oamd_stamps[kMaxStampWgs * 16];
+__device__ unsigned long long g_oamd_stamps[kMaxStampWgs * kStampStride];
 __device__ __forceinline__ void stamp(int slot, int wave, int lane) {
     if (wave == 0 && lane == 0 && blockIdx.x < kMaxStampWgs) {
         __builtin_amdgcn_sched_barrier(0);
-        g_oamd_stamps[blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
-        if (slot == 1 || slot == 2) g_oamd_stamps[blockIdx.x * 16 + 4 + slot] = __builtin_amdgcn_s_memtime();
+        g_oamd_stamps[blockIdx.x * kStampStride + slot] = __builtin_amdgcn_s_memrealtime();
+        if (slot == 1 || slot == 2) g_oamd_stamps[blockIdx.x * kStampStride + 4 + slot] = __builtin_amdgcn_s_memtime();
         if (slot == 0) {
             unsigned id;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(id));
             unsigned xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            g_oamd_stamps[blockIdx.x * 16 + 4] = ((unsigned long long)xcc << 32) | id;
+            g_oamd_stamps[blockIdx.x * kStampStride + 4] = ((unsigned long long)xcc << 32) | id;
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -701,6 +706,14 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
 #ifdef OAMD_STAMPS
     // epilogue cycle sums: first barrier, stores, second barrier + first reads
     unsigned long long ep_sum[3] = {0, 0, 0}, ep_t = 0;
+    unsigned long long wt_sum[3] = {0, 0, 0};  // lgkmcnt, vmcnt, stage barrier waits
+    // a step's stamps (s_memtime, an SMEM read counted in lgkmcnt) are read
+    // only after the NEXT step's lgkmcnt(0), which the kernel waits for anyway:
+    // consuming one earlier would drain the fragment reads in flight and
+    // change what is measured. pw[0] = before the step's lgkmcnt(0), [1]
+    // after it, [2] after the stage-open vmcnt wait, [3] after the barrier
+    unsigned long long pw[4] = {0, 0, 0, 0};
+    bool pw_on = false, pw_open = false;
 #define OAMD_EP_MARK(k)                                                          \
     do {                                                                         \
         __builtin_amdgcn_sched_barrier(0);                                       \
@@ -709,8 +722,41 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         ep_t = t_;                                                               \
         __builtin_amdgcn_sched_barrier(0);                                       \
     } while (0)
+#define OAMD_T() __builtin_amdgcn_s_memtime()
+#define OAMD_STEP_WAIT(stmt)                                                     \
+    do {                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                       \
+        const unsigned long long w0_ = OAMD_T();                                 \
+        stmt;                                                                    \
+        if (pw_on) {                                                             \
+            wt_sum[0] += pw[1] - pw[0];                                          \
+            if (pw_open) {                                                       \
+                wt_sum[1] += pw[2] - pw[1];                                      \
+                wt_sum[2] += pw[3] - pw[2];                                      \
+            }                                                                    \
+        }                                                                        \
+        pw[0] = w0_;                                                             \
+        pw[1] = OAMD_T();                                                        \
+        pw_on = true;                                                            \
+        pw_open = false;                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                       \
+    } while (0)
+#define OAMD_OPEN_WAIT(vmstmt, barstmt)                                          \
+    do {                                                                         \
+        vmstmt;                                                                  \
+        pw[2] = OAMD_T();                                                        \
+        barstmt;                                                                 \
+        pw[3] = OAMD_T();                                                        \
+        pw_open = true;                                                          \
+    } while (0)
 #else
 #define OAMD_EP_MARK(k) ((void)0)
+#define OAMD_STEP_WAIT(stmt) stmt
+#define OAMD_OPEN_WAIT(vmstmt, barstmt) \
+    do {                                 \
+        vmstmt;                          \
+        barstmt;                         \
+    } while (0)
 #endif
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(N.w);
 
@@ -869,6 +915,9 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     for (int m = kWide ? 1 : 0; m < kMT; ++m)
         fa.x[m] = *reinterpret_cast<const u32x4_t*>(act + first_kstep_offset<C>(0) + rd[m]);
     OAMD_STAMP(1);
+#ifdef OAMD_STAMPS
+    const unsigned long long tower_t0 = __builtin_amdgcn_s_memtime();
+#endif
     // throughput geometry: every ResNet wave issues ahead of the other pipeline
     // group's co-resident tree waves (SQ arbitration): bench C2 4.42-4.47 vs
     // 4.31-4.36 M sims/s (four same-box pairs on two boxes), launch 0.90-0.91
@@ -921,7 +970,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             // cur's reads (issued a step ago) are done: retire them before
             // issuing nxt's, or 16 outstanding reads overflow the 4-bit lgkmcnt
             // and the compiler drains nxt's reads too
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+            OAMD_STEP_WAIT(__builtin_amdgcn_s_waitcnt(0xC07F));  // lgkmcnt(0)
             // activation fragments do not depend on the stage barrier (the
             // layer's input is fixed): issued before it, their latency overlaps
             // the barrier wait (+3.6 %)
@@ -934,8 +983,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 // open the next stage: it has landed (this wave's DMAs, then
                 // everyone's via the barrier), and the slot of the stage before the
                 // current one is drained by all waves: the newest stage goes there
-                wait_vm<G::VM_OPEN>();
-                __builtin_amdgcn_s_barrier();
+                OAMD_OPEN_WAIT(wait_vm<G::VM_OPEN>(), __builtin_amdgcn_s_barrier());
                 const int sp = (slot + G::AHEAD + 1) % G::RING;  // (g + 1 + AHEAD) % RING
                 wcur += G::STAGE;
                 issue_stage_dma<G, G::OPEN_PART>(wcur, ring, sp, tid);
@@ -1036,15 +1084,14 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                     if constexpr (cbn % 2 == 0) return win0; else return win1;
                 }();
                 __builtin_amdgcn_sched_barrier(0);
-                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wc / Wc have landed
+                OAMD_STEP_WAIT(__builtin_amdgcn_s_waitcnt(0xC07F));  // lgkmcnt(0): wc / Wc have landed
                 static_for<9>([&](auto I) {
                     constexpr int i = decltype(I)::value;
                     if constexpr ((wide_new(Jn) >> i) & 1)
                         Wn[i] = *reinterpret_cast<const u32x4_t*>(act + sbn + i * RS + cbn * 64);
                 });
                 if constexpr (open) {
-                    wait_vm<G::VM_OPEN>();
-                    __builtin_amdgcn_s_barrier();
+                    OAMD_OPEN_WAIT(wait_vm<G::VM_OPEN>(), __builtin_amdgcn_s_barrier());
                     const int sp = (slot + G::AHEAD + 1) % G::RING;
                     wcur += G::STAGE;
                     issue_stage_dma<G, G::OPEN_PART>(wcur, ring, sp, tid);
@@ -1123,6 +1170,11 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         // loaded before the next DMA so the counted wait below covers it
         const bool more = layer + 1 < nlayers;
         if (more) load_bias<G>(bv, N, layer + 1, wn, lane);
+#ifdef OAMD_STAMPS
+        // the layer's last step: its stamps are complete once the epilogue mark waits
+        OAMD_STEP_WAIT(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"));
+        pw_on = false;
+#endif
         OAMD_EP_MARK(0);
         lds_barrier();  // every wave is done reading this layer's input and its last stage
         OAMD_EP_MARK(1);
@@ -1184,8 +1236,17 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     __syncthreads();  // also drains this wave's trailing ring DMAs: the ring is free
     OAMD_STAMP(2);
 #ifdef OAMD_STAMPS
+    const unsigned long long tower_cyc = __builtin_amdgcn_s_memtime() - tower_t0;
+#endif
+#ifdef OAMD_STAMPS
     if (wave == 0 && lane == 0 && blockIdx.x < kMaxStampWgs)
-        for (int i = 0; i < 3; ++i) g_oamd_stamps[blockIdx.x * 16 + 11 + i] = ep_sum[i];
+        for (int i = 0; i < 3; ++i) g_oamd_stamps[blockIdx.x * kStampStride + 11 + i] = ep_sum[i];
+    if (lane == 0 && blockIdx.x < kMaxStampWgs) {
+        unsigned long long* q = g_oamd_stamps + blockIdx.x * kStampStride + 16;
+        for (int i = 0; i < 3; ++i) atomicAdd(q + i, wt_sum[i]);
+        for (int i = 0; i < 3; ++i) atomicAdd(q + 3 + i, ep_sum[i]);
+        atomicAdd(q + 6, tower_cyc);
+    }
 #endif
     heads<G, DT>(N, act, ring, wave, lane, row0, M, policy, value);
     OAMD_STAMP(3);
@@ -1275,7 +1336,7 @@ void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* pol
 
 int resnet_read_stamps(unsigned long long* out, long long n) {
 #ifdef OAMD_STAMPS
-    if (n > (long long)kMaxStampWgs * 16) n = (long long)kMaxStampWgs * 16;
+    if (n > (long long)kMaxStampWgs * kStampStride) n = (long long)kMaxStampWgs * kStampStride;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oamd_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
                ? 0
                : -1;

@@ -20,16 +20,18 @@ import othello_mcts as om  # noqa: E402
 from othello_mcts.synthetic import alphazero_state_dict  # noqa: E402
 
 rows = int(os.environ.get("ROWS", "8192"))
-net = om.NativeNet(alphazero_state_dict(1, 17, 128, 9, 128), device=0)
+dtype = os.environ.get("NN_DTYPE", "bf16")
+net = om.NativeNet(alphazero_state_dict(1, 17, 128, 9, 128), device=0, dtype=dtype)
 x = (torch.rand((rows, 17, 8, 8), device="cuda") < 0.3).float()
 for _ in range(20):
     net(x)
 torch.cuda.synchronize()
 lib = ctypes.CDLL(str(ROOT / "othello-alphazero_amd" / "othello_mcts" / "liboamd.so"))
 wgs = rows // 4
-buf = (ctypes.c_uint64 * (wgs * 16))()
-assert lib.oamd_debug_read_stamps(buf, ctypes.c_int64(wgs * 16)) == 0, "build with -DOAMD_STAMPS"
-s = np.frombuffer(buf, dtype=np.uint64).reshape(wgs, 16).astype(np.int64)
+STRIDE = 24  # resnet.hip kStampStride
+buf = (ctypes.c_uint64 * (wgs * STRIDE))()
+assert lib.oamd_debug_read_stamps(buf, ctypes.c_int64(wgs * STRIDE)) == 0, "build with -DOAMD_STAMPS"
+s = np.frombuffer(buf, dtype=np.uint64).reshape(wgs, STRIDE).astype(np.int64)
 t0, t1, t2, t3, hw, c1, c2, t7, h0, h1, h2, e0, e1, e2 = (s[:, i] for i in range(14))
 cu_key = ((hw >> 32) << 8) | ((hw >> 8) & 0xFF)  # XCC id, SE/SH/CU fields of HW_ID
 ns = 10.0  # s_memrealtime: 100 MHz
@@ -72,3 +74,10 @@ if e0.any():
     print(f"epilogues (19 per tower, share of tower cycles, median): first barrier {np.median(e0 / tc):.2%}, "
           f"stores {np.median(e1 / tc):.2%}, second barrier + next layer's first reads {np.median(e2 / tc):.2%}")
 print(f"tower clock (s_memtime / s_memrealtime): median {np.median(clk):.3f} GHz")
+# all 8 waves' cycle sums (slots 16-22): where a wave's tower time goes
+wsum = s[:, 16:23].sum(axis=0).astype(float)
+if wsum[6] > 0:
+    names = ["step-start lgkmcnt(0) (fragment reads)", "stage-open vmcnt (weight DMA)", "stage barrier",
+             "epilogue first barrier", "epilogue stores", "epilogue second barrier + first reads"]
+    print("share of the 8 waves' tower cycles: " + ", ".join(f"{n} {wsum[i] / wsum[6]:.2%}" for i, n in enumerate(names))
+          + f"; rest (MFMA issue, fragment-read issue, VALU) {1 - wsum[:6].sum() / wsum[6]:.2%}")

@@ -169,9 +169,18 @@ def bench_summary(outdir: str, prefix: str, tag: str) -> dict:
             for ln in log.read_text().splitlines():
                 if ln.startswith("{") and '"metric"' in ln:
                     bench = json.loads(ln)
-    # the NN rows a launch evaluates on average (the bench line's n_eval per
-    # launch: evaluation lists and the small extra chain-splitting rounds)
-    rows = bench["roofline"].get("n_eval_per_launch", bench["roofline"]["rows_per_launch"]) if bench else None
+    # the NN rows a regular launch evaluates (the per-launch counters above
+    # skip the chain-splitting extra rounds' near-empty launches): the bench
+    # line's n_eval over the regular rounds' launches (the extra rounds
+    # evaluate lagging games only, none outside endgames)
+    rows = None
+    if bench:
+        r, cfg = bench["roofline"], bench["config"]
+        rounds = bench["tree_kernels"].get("rounds_per_search")
+        regular = -(-cfg["sims_per_move"] // cfg["leaves_per_step"])
+        launches = r.get("launches") or r.get("timed_region_launches")
+        rows = (bench["work"]["n_eval"] / (launches * regular / rounds) if rounds and launches
+                else r.get("n_eval_per_launch", r["rows_per_launch"]))
     fpr = bench["roofline"]["flops_per_row"] if bench else None
     res = {"tag": tag, "source": f"tools/gpu.sh pmc {prefix}_* over bench.py",
            "workload": bench["config"]["workload"] if bench else None,
