@@ -339,6 +339,8 @@ def parse_args(argv: list[str]):
                     help="re-selections after all-terminal batches per game and round before the chain is split "
                          "(0 = never split; exact interleaving only)")
     ap.add_argument("--chain-cuts", type=int, default=8, help="chain splits per game and search (= extra rounds)")
+    ap.add_argument("--extra-grid", type=int, default=128,
+                    help="workgroups of the extra rounds' ResNet launches (0 = the regular grid)")
     ap.add_argument("--cpu-baseline-moves", type=int, default=24,
                     help="timed moves of the CPU baseline (0 = skip it), after 2 warm-up moves")
     ap.add_argument("--cpu-baseline-threads", type=int, default=0,
@@ -435,6 +437,7 @@ class EngineWorkload:
         self.b.engine.set_nn_chains(args.nn_chains)
         self.b.engine.set_exact_interleaving(not args.round_robin_endgames)
         self.b.engine.set_chain_split(args.chain_budget, args.chain_cuts)
+        self.b.engine.set_extra_round_grid(args.extra_grid)
         props = torch.cuda.get_device_properties(local)
         self.device_id = f"{os.uname().nodename}:{getattr(props, 'uuid', local)}"
 

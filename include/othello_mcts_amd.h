@@ -196,6 +196,12 @@ int oamd_engine_set_chain_split(oamd_engine *e, int32_t budget, int32_t cuts);
  * search rounds stay hidden behind the other pipeline group's ResNet launch
  * in sustained self-play. */
 int oamd_engine_set_exact_interleaving(oamd_engine *e, int32_t enable);
+/* Workgroups of the chain-splitting extra rounds' ResNet launches (default
+ * 128; 0 = the regular grid, the list's capacity): those launches hold the
+ * rows of lagging games only (none outside endgames), so a small grid loops
+ * over them instead of dispatching ~1000 mostly empty workgroups between the
+ * other NN chain's. Scheduling only: results are identical. */
+int oamd_engine_set_extra_round_grid(oamd_engine *e, int32_t workgroups);
 /* Diagnostics: copy the ResNet kernel's per-workgroup time stamps (8 u64 per
  * workgroup, 16 u64 per workgroup: see tools/nn_stamps.py) of the last launch. Only in builds
  * with OAMD_EXTRA_FLAGS=-DOAMD_STAMPS; otherwise OAMD_INVALID_ARGUMENT. */

@@ -173,6 +173,8 @@ struct oamd_engine {
     // search (k_tree); chain_cuts extra rounds per search. 0 = never split
     int chain_budget = 4;
     int chain_cuts = 8;
+    // workgroups of an extra round's ResNet launch (0 = the regular grid)
+    int extra_grid = 128;
     int step_phase = 0;  // 1 = a selected round awaits its backup (step API)
     // pipeline groups (0 = auto) and their streams / fork-join events
     int pipeline = 0;
@@ -1103,10 +1105,12 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
             if (ev) HIPCHK(hipEventRecord(ev[2], ns));
             const int grows = P.ng[k] * L;
             const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
+            // the extra rounds evaluate lagging games only: a small looping grid
+            const int max_wgs = s >= steps ? e->extra_grid : 0;
             for (int r = 0, j = 0; r < grows; r += cb, ++j)
                 launch_resnet_packed(N, E.feat, E.FW, E.H, std::min(cb, grows - r), E.policy, E.value, ns,
                                      E.rowlist + r0 + r, cnt + (s & 1), r,
-                                     span ? span + (size_t)2 * ((k * S + s) * nlg + j) : nullptr);
+                                     span ? span + (size_t)2 * ((k * S + s) * nlg + j) : nullptr, max_wgs);
             if (ev) HIPCHK(hipEventRecord(ev[3], ns));
             if (K > 1 && OAMD_NN_ORDER == 2) {
                 HIPCHK(hipEventRecord(e->nn_ev[k], ns));
@@ -1249,6 +1253,12 @@ int oamd_engine_set_chain_split(oamd_engine* e, int32_t budget, int32_t cuts) {
     if (budget < 0 || cuts < 0 || cuts > 64) return fail(OAMD_INVALID_ARGUMENT, "chain split: budget >= 0, cuts in [0, 64]");
     e->chain_budget = budget;
     e->chain_cuts = cuts;
+    return OAMD_OK;
+}
+
+int oamd_engine_set_extra_round_grid(oamd_engine* e, int32_t workgroups) {
+    if (workgroups < 0) return fail(OAMD_INVALID_ARGUMENT, "extra-round grid must be >= 0");
+    e->extra_grid = workgroups;
     return OAMD_OK;
 }
 

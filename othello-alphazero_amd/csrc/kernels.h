@@ -67,13 +67,15 @@ struct NetView {
 // Packed rows with an evaluation list (rowlist != nullptr): the launch
 // evaluates rows rowlist[0 .. min(rows, *rowcount - list_off)) (absolute row
 // indices into feat / policy / value); without one, rows 0 .. rows-1.
+// max_wgs > 0: at most that many workgroups, looping over the board groups
+// (the chain-splitting extra rounds' nearly empty launches).
 // span != nullptr (timed searches): the launch records its execution interval
 // in span[0] = ~(earliest workgroup start), span[1] = latest workgroup end
 // (s_memrealtime, 100 MHz ticks; zero-initialised by the caller)
 void launch_resnet_packed(const NetView& N, const uint64_t* feat, int fw, int H, int rows,
                           float* policy, float* value, hipStream_t s, const int32_t* rowlist = nullptr,
                           const int32_t* rowcount = nullptr, int list_off = 0,
-                          unsigned long long* span = nullptr);
+                          unsigned long long* span = nullptr, int max_wgs = 0);
 void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* policy, float* value,
                        hipStream_t s);
 size_t resnet_packed_weight_elems(int C, int R);

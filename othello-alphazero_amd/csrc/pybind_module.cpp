@@ -666,6 +666,8 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
         .def("set_pipeline", [](Engine& e, int groups) { check(oamd_engine_set_pipeline(e.h, groups)); })
         .def("set_nn_batch", [](Engine& e, int rows) { check(oamd_engine_set_nn_batch(e.h, rows)); })
         .def("set_nn_chains", [](Engine& e, int chains) { check(oamd_engine_set_nn_chains(e.h, chains)); })
+        .def("set_extra_round_grid",
+             [](Engine& e, int workgroups) { check(oamd_engine_set_extra_round_grid(e.h, workgroups)); })
         .def("set_chain_split",
              [](Engine& e, int budget, int cuts) { check(oamd_engine_set_chain_split(e.h, budget, cuts)); })
         .def("set_exact_interleaving",

@@ -680,7 +680,7 @@ __device__ __forceinline__ void load_bias(float4 (&bv)[G::NT], const NetView& N,
 
 template <class G, int DT, int IN>
 __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ feat_in, int fw, int H, RowMap M,
-                                            float* __restrict__ policy, float* __restrict__ value) {
+                                            float* __restrict__ policy, float* __restrict__ value, int wg) {
     constexpr int C = G::C;
     constexpr int kNT = G::NT;
     constexpr int kMT = G::MT;
@@ -694,7 +694,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
     const int wm = wave / G::WN;  // position group of this wave (EDGE: edge_tile_row; else its board)
     const int wn = wave % G::WN;  // 32-channel block of this wave
     const int kg = lane >> 4;
-    const int row0 = blockIdx.x * G::BOARDS;
+    const int row0 = wg * G::BOARDS;  // this workgroup's first board of the launch
     if (M.list) {  // entries filled this round (a uniform scalar load)
         const int filled = *M.count - M.off;
         M.rows = filled < M.rows ? (filled > 0 ? filled : 0) : M.rows;
@@ -1268,7 +1268,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_vgpr(OAMD_VGPR_CAP))
     // endgame launches nobody overlaps make visible). Every early return of
     // resnet_body is workgroup-uniform, so all threads meet at the barrier.
     if (M.span && threadIdx.x == 0) atomicMax(M.span, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
-    resnet_body<G, DT, IN>(N, feat_in, fw, H, M, policy, value);
+    resnet_body<G, DT, IN>(N, feat_in, fw, H, M, policy, value, blockIdx.x);
+    if (M.span) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(M.span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+}
+
+// The chain-splitting extra rounds' launches (lagging games' rows only, none
+// outside endgames) on a small grid that loops over the list's board groups:
+// the regular grid (the list's capacity, ~1000 workgroups of 139 KB of LDS)
+// would put each of its empty workgroups on a CU for a moment, between the
+// other NN chain's workgroups. Same per-board arithmetic, bit-identical.
+template <class G, int DT, int IN>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_num_vgpr(OAMD_VGPR_CAP))) void k_resnet_w8_loop(
+    NetView N, const void* __restrict__ feat_in, int fw, int H, RowMap M, float* __restrict__ policy,
+    float* __restrict__ value) {
+    if (M.span && threadIdx.x == 0) atomicMax(M.span, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+    int rows = M.rows;
+    if (M.list) {
+        const int filled = *M.count - M.off;
+        rows = filled < rows ? (filled > 0 ? filled : 0) : rows;
+    }
+    for (int wg = blockIdx.x; wg * G::BOARDS < rows; wg += gridDim.x) {
+        resnet_body<G, DT, IN>(N, feat_in, fw, H, M, policy, value, wg);
+        __syncthreads();  // the heads' scratch (the drained ring) is read before the next group's DMA
+    }
     if (M.span) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(M.span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1277,7 +1302,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_num_vgpr(OAMD_VGPR_CAP))
 
 template <class G, int DT, int IN>
 static void launch_t(const NetView& N, const void* feat, int fw, int H, const RowMap& M, float* pol, float* val,
-                     hipStream_t s) {
+                     hipStream_t s, int max_wgs) {
     const int rows = M.rows;
     static_assert(G::THREADS == 512, "k_resnet_w8 geometries");
     const unsigned grid = (unsigned)((rows + G::BOARDS - 1) / G::BOARDS);
@@ -1287,6 +1312,19 @@ static void launch_t(const NetView& N, const void* feat, int fw, int H, const Ro
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   G::LDS);
         configured = true;
+    }
+    if constexpr (IN == kPacked) {
+        if (max_wgs > 0 && grid > (unsigned)max_wgs) {
+            constexpr auto lk = &k_resnet_w8_loop<G, DT, IN>;
+            static bool lconfigured = false;
+            if (!lconfigured) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lk),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+                lconfigured = true;
+            }
+            hipLaunchKernelGGL(lk, dim3(max_wgs), dim3(G::THREADS), G::LDS, s, N, feat, fw, H, M, pol, val);
+            return;
+        }
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G::THREADS), G::LDS, s, N, feat, fw, H, M, pol, val);
 }
@@ -1299,34 +1337,34 @@ constexpr int kSmallBatchRows = 1024;
 
 template <int IN>
 static void dispatch(const NetView& N, const void* feat, int fw, int H, const RowMap& M, float* pol, float* val,
-                     hipStream_t s) {
+                     hipStream_t s, int max_wgs = 0) {
     const int rows = M.rows;
     if (rows <= 0) return;
     const bool small = rows < kSmallBatchRows;
     const bool fp16 = N.dtype == OAMD_FP16;
     if (N.C == 128) {
         if (small) {
-            if (fp16) launch_t<GeoS<128>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s);
-            else launch_t<GeoS<128>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s);
+            if (fp16) launch_t<GeoS<128>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s, max_wgs);
+            else launch_t<GeoS<128>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s, max_wgs);
         } else {
-            if (fp16) launch_t<Geo<128>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s);
-            else launch_t<Geo<128>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s);
+            if (fp16) launch_t<Geo<128>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s, max_wgs);
+            else launch_t<Geo<128>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s, max_wgs);
         }
     } else {
         if (small) {
-            if (fp16) launch_t<GeoS<256>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s);
-            else launch_t<GeoS<256>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s);
+            if (fp16) launch_t<GeoS<256>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s, max_wgs);
+            else launch_t<GeoS<256>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s, max_wgs);
         } else {
-            if (fp16) launch_t<Geo<256>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s);
-            else launch_t<Geo<256>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s);
+            if (fp16) launch_t<Geo<256>, OAMD_FP16, IN>(N, feat, fw, H, M, pol, val, s, max_wgs);
+            else launch_t<Geo<256>, OAMD_BF16, IN>(N, feat, fw, H, M, pol, val, s, max_wgs);
         }
     }
 }
 
 void launch_resnet_packed(const NetView& N, const uint64_t* feat, int fw, int H, int rows,
                           float* policy, float* value, hipStream_t s, const int32_t* rowlist,
-                          const int32_t* rowcount, int list_off, unsigned long long* span) {
-    dispatch<kPacked>(N, feat, fw, H, RowMap{rowlist, rowcount, list_off, rows, span}, policy, value, s);
+                          const int32_t* rowcount, int list_off, unsigned long long* span, int max_wgs) {
+    dispatch<kPacked>(N, feat, fw, H, RowMap{rowlist, rowcount, list_off, rows, span}, policy, value, s, max_wgs);
 }
 
 void launch_resnet_f32(const NetView& N, const float* feat, int rows, float* policy, float* value,

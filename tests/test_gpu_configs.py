@@ -299,10 +299,14 @@ def test_chain_split_keeps_every_game_identical(om):
     net = om.NativeNet(alphazero_state_dict(43, 9, 128, 1, 32), device=0)
     kw = dict(history_size=4, num_simulations=320, num_threads=2, batch_size=16, dirichlet_epsilon=0.25, seed=8,
               node_capacity=1 << 17)
-    splits = [(0, 0), (1, 3), (4, 4)]
+    # (budget, cuts, extra-round grid): the extra rounds' ResNet launches loop
+    # over the lagging games' rows on a small grid (1 workgroup: every board
+    # group in turn) or use the regular grid (0)
+    splits = [(0, 0, 128), (1, 3, 128), (4, 4, 128), (4, 8, 1), (1, 8, 0)]
     engines = [om.BatchedMCTS(64, **kw) for _ in splits]
-    for x, (budget, cuts) in zip(engines, splits):
+    for x, (budget, cuts, grid) in zip(engines, splits):
         x.engine.set_chain_split(budget, cuts)
+        x.engine.set_extra_round_grid(grid)
     ref = om.BatchedMCTS(64, **kw)
     for x in engines + [ref]:
         x.random_openings(50, seed=9)
@@ -321,7 +325,7 @@ def test_chain_split_keeps_every_game_identical(om):
             assert torch.equal(o["actions"], xr["actions"]) and torch.equal(o["finished"], xr["finished"]), (mv, sp)
     share = 1.0 - total_evals / total_sims
     numerics.record("chain split", f"64 late games x 24 moves: terminal-leaf share {share:.3f}, "
-                                   "budgets 0/1/4 == callback")
+                                   "budgets 0/1/4, extra-round grids 1/128/regular == callback")
     assert share > 0.1
 
 
