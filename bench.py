@@ -90,28 +90,15 @@ def single_game_split(args) -> bool:
     return args.games == 1 and pipeline_groups(args) == 1 and 1 < args.threads <= 8
 
 
-def search_rounds(args) -> int:
-    """NN rounds of one native search (capi.hip search_rounds): one per batch of
-    a thread, plus the chain-splitting extra rounds (exact interleaving only)."""
+def max_search_rounds(args) -> int:
+    """The most NN rounds one native search runs: one per batch of a thread,
+    plus up to chain_cuts extra rounds (exact interleaving only; the engine
+    picks each search's count adaptively, capi.hip pick_extra_rounds, and
+    reports the rounds it ran: oamd_engine_round_counts)."""
     steps = (args.sims + args.threads * args.batch - 1) // (args.threads * args.batch)
     extra = args.chain_cuts if (not args.round_robin_endgames and args.chain_budget > 0
                                 and not single_game_split(args)) else 0
     return steps + extra
-
-
-def timed_region_resnet_launches(args) -> int:
-    """k_resnet dispatches of the timed region (all rounds of every search): the
-    trace cross-check (tools/prof_summary.py) takes the last this many."""
-    if single_game_split(args):
-        return args.steps * search_rounds(args) * args.threads
-    K = pipeline_groups(args)
-    L = args.threads * args.batch
-    n = 0
-    for k in range(K):
-        grows = (args.games * (k + 1) // K - args.games * k // K) * L
-        cb = args.eval_batch if args.eval_batch > 0 else grows
-        n += (grows + cb - 1) // cb
-    return args.steps * search_rounds(args) * n
 
 
 def resnet_flops_per_eval(in_ch: int, C: int, R: int, hidden: int) -> float:
@@ -338,7 +325,10 @@ def parse_args(argv: list[str]):
     ap.add_argument("--chain-budget", type=int, default=4,
                     help="re-selections after all-terminal batches per game and round before the chain is split "
                          "(0 = never split; exact interleaving only)")
-    ap.add_argument("--chain-cuts", type=int, default=8, help="chain splits per game and search (= extra rounds)")
+    ap.add_argument("--chain-cuts", type=int, default=16,
+                    help="most chain splits per game and search (= most extra rounds)")
+    ap.add_argument("--adaptive-min", type=int, default=2,
+                    help="fewest extra rounds of the adaptive count (0 = always --chain-cuts)")
     ap.add_argument("--extra-grid", type=int, default=128,
                     help="workgroups of the extra rounds' ResNet launches (0 = the regular grid)")
     ap.add_argument("--cpu-baseline-moves", type=int, default=24,
@@ -438,6 +428,7 @@ class EngineWorkload:
         self.b.engine.set_exact_interleaving(not args.round_robin_endgames)
         self.b.engine.set_chain_split(args.chain_budget, args.chain_cuts)
         self.b.engine.set_extra_round_grid(args.extra_grid)
+        self.b.engine.set_adaptive_extra_rounds(args.adaptive_min)
         props = torch.cuda.get_device_properties(local)
         self.device_id = f"{os.uname().nodename}:{getattr(props, 'uuid', local)}"
 
@@ -463,20 +454,21 @@ class EngineWorkload:
     def start_measuring(self, every: int | None = None) -> None:
         e = self.b.engine
         e.enable_timing(max(1, self.args.timing_every if every is None else every))
-        self.t0 = (e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy())
+        self.t0 = (e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy(), e.round_counts())
 
     def stop_measuring(self) -> dict:
         e = self.b.engine
-        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), (bu0, bl0) = self.t0
-        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), (bu1, bl1) = (e.nn_timing(), e.tree_timing(),
-                                                                    e.work_counters(), e.nn_busy())
+        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), (bu0, bl0), (sc0, ro0, fl0) = self.t0
+        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), (bu1, bl1), (sc1, ro1, fl1) = (
+            e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy(), e.round_counts())
         overflow_games, depth_capped = e.status()
         if overflow_games or depth_capped:
             raise SystemExit(f"bench invalid: {overflow_games} game(s) overflowed their node pool, "
                              f"{depth_capped} hit the depth cap")
         return {"nn_ms": ms1 - ms0, "nn_busy_ms": bu1 - bu0, "busy_launches": bl1 - bl0, "nn_launches": la1 - la0,
                 "nn_rows": rw1 - rw0, "select_ms": se1 - se0,
-                "backup_ms": bk1 - bk0, "tree_launches": tl1 - tl0, "sims": si1 - si0, "evals": ev1 - ev0,
+                "backup_ms": bk1 - bk0, "tree_launches": tl1 - tl0, "final_launches": fl1 - fl0,
+                "searches": sc1 - sc0, "rounds": ro1 - ro0, "sims": si1 - si0, "evals": ev1 - ev0,
                 "overflow_games": overflow_games}
 
 
@@ -549,6 +541,9 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
             "backend": (backend if grouped() else "none"),
             "endgame_interleaving": ("round-robin" if args.round_robin_endgames else
                                      f"exact (reference), chains split after {args.chain_budget} re-selections, "
+                                     f"<= X times per search, X extra rounds, X adaptive in "
+                                     f"[{min(args.adaptive_min, args.chain_cuts)}, {args.chain_cuts}]"
+                                     if args.adaptive_min > 0 else
                                      f"<= {args.chain_cuts} times per search"),
             "calls": ("search + selfplay_move per step" if args.per_move_calls or args.sync_search
                       else f"one selfplay_steps call for the {args.steps} timed steps"),
@@ -650,11 +645,13 @@ def measured_fields(args, m: dict, workload: str) -> dict:
             tree_bytes = {}
     # k_tree: one launch per search round and pipeline group; "select" rounds
     # back up the previous batch and select the next, the final round backs up
-    tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch), "rounds_per_search": search_rounds(args)}
-    # timed rounds per search: every selecting round (the chain-splitting extra
-    # rounds included) + the final backup
+    # rounds per search: every selecting round (the chain-splitting extra
+    # rounds included; their count adapts per search) + the final backup
+    rounds = m["rounds"] / m["searches"] if m.get("searches") else float(max_search_rounds(args))
+    tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch), "rounds_per_search": round(rounds, 3),
+            "max_rounds_per_search": max_search_rounds(args)}
     for name, ms, n in (("k_tree", m["select_ms"], m["tree_launches"]),
-                        ("k_tree_final_backup", m["backup_ms"], m["tree_launches"] // search_rounds(args))):
+                        ("k_tree_final_backup", m["backup_ms"], m["final_launches"])):
         avg = ms / max(1, n)
         entry = {"avg_launch_ms": round(avg, 4)}
         if name in tree_bytes:
@@ -678,7 +675,7 @@ def measured_fields(args, m: dict, workload: str) -> dict:
                       "x flops_per_row / busy ms per launch (the union of the kernel-recorded execution intervals "
                       "of every ResNet launch in the timed region / those launches)"),
             "launches": m["busy_launches"],
-            "timed_region_launches": timed_region_resnet_launches(args),
+            "timed_region_launches": m["busy_launches"],
             "kernel_hash": kernel_hash("resnet"),
             "avg_launch_ms": round(avg_ms, 4),
             "busy_ms_per_launch": round(busy_ms, 4),

@@ -184,9 +184,24 @@ int oamd_engine_set_nn_chains(oamd_engine *e, int32_t chains);
  * re-selections in a round such a chain stops and the game's next round
  * resumes it exactly there (every game keeps its order of operations; only
  * round boundaries move), at most `cuts` times per search, at the cost of
- * `cuts` extra rounds per search. Default budget 8, cuts 3; budget 0 = never
- * split. Results do not depend on it. */
+ * up to `cuts` extra rounds per search (see the adaptive count below).
+ * Default budget 4, cuts 16; budget 0 = never split. Results do not depend on
+ * it. */
 int oamd_engine_set_chain_split(oamd_engine *e, int32_t budget, int32_t cuts);
+/* Adaptive extra rounds (default min_rounds 2): a grouped native search runs
+ * X extra rounds and allows X cuts per game, X in [min(min_rounds, cuts),
+ * cuts], following the most cuts u any game used two searches earlier (X =
+ * u + 2, or twice that search's X when u reached it; read back without
+ * draining the queue). Extra rounds past every game's last cut are empty
+ * launches; a game that would need more cuts runs its last chain uncut.
+ * min_rounds = 0: X = cuts always. Scheduling only: results are identical. */
+int oamd_engine_set_adaptive_extra_rounds(oamd_engine *e, int32_t min_rounds);
+/* Counts since the engine was created: grouped native searches enqueued (all
+ * pipeline groups of one search count once), their NN rounds (steps + extra
+ * rounds each), and the final backup-only k_tree launches of the timed
+ * searches (the launches behind oamd_engine_tree_timing's backup_ms). */
+int oamd_engine_round_counts(const oamd_engine *e, int64_t *searches, int64_t *rounds,
+                             int64_t *final_launches);
 /* enable = 1 (default): the reference's thread interleaving exactly — a
  * virtual thread whose batch is all terminal backs it up without an NN round
  * trip and selects again at once (search_thread.cpp:102-127), in the same

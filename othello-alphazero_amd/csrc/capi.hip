@@ -172,7 +172,28 @@ struct oamd_engine {
     // chain_budget re-selections in a round, at most chain_cuts times per
     // search (k_tree); chain_cuts extra rounds per search. 0 = never split
     int chain_budget = 4;
-    int chain_cuts = 8;
+    int chain_cuts = 16;
+    // adaptive extra rounds (pick_extra_rounds): a grouped search runs X in
+    // [min(adapt_min, chain_cuts), chain_cuts] extra rounds (and allows X
+    // cuts), X following the most cuts any game used two searches earlier.
+    // adapt_min = 0: always chain_cuts
+    static constexpr int kCutSlots = 4;
+    int adapt_min = 2;
+    int adapt_x = 0;         // the last X picked from a measurement (0: none yet)
+    int64_t adapt_seq = 0;   // grouped searches enqueued with a cuts slot
+    int32_t* cuts_dev = nullptr;   // [kCutSlots][kMaxPipeline] most cuts per search and group
+    int32_t* cuts_host = nullptr;  // pinned copies
+    int cut_x[kCutSlots] = {};     // X of the search in the slot (0: slot empty)
+    int cut_groups[kCutSlots] = {};
+    hipEvent_t cuts_ev[kCutSlots][kMaxPipeline] = {};
+    int ensure_cut_slots() {
+        if (cuts_dev) return OAMD_OK;
+        if (int rc = dalloc(&cuts_dev, (size_t)kCutSlots * kMaxPipeline)) return rc;
+        HIPCHK(hipHostMalloc((void**)&cuts_host, sizeof(int32_t) * kCutSlots * kMaxPipeline));
+        for (auto& row : cuts_ev)
+            for (auto& x : row) HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+        return OAMD_OK;
+    }
     // workgroups of an extra round's ResNet launch (0 = the regular grid)
     int extra_grid = 128;
     int step_phase = 0;  // 1 = a selected round awaits its backup (step API)
@@ -219,13 +240,14 @@ struct oamd_engine {
     static constexpr int64_t kSpanChunk = 1 << 15;  // slots (2 x u64) per chunk
     std::vector<unsigned long long*> span_chunks;
     int64_t span_used = 0;      // slot index where the next search's block starts
-    int64_t span_launches = 0;  // slots handed out in the window
     int ev_cur = 0;
     float nn_ms = 0.0f;
     float select_ms = 0.0f;
     float backup_ms = 0.0f;
     int64_t nn_launches = 0;
     int64_t tree_launches = 0;  // timed select rounds (one k_tree launch per round and group)
+    int64_t tree_final_launches = 0;  // timed final backup-only rounds (x groups)
+    int64_t grouped_searches = 0, grouped_rounds = 0;  // oamd_engine_round_counts
     int64_t nn_rows = 0;
 
     int resolve_timing(int p) {
@@ -252,6 +274,7 @@ struct oamd_engine {
 
         nn_launches += ev_launches[p];
         tree_launches += ev_final[p];
+        tree_final_launches += n - ev_final[p];
         nn_rows += ev_rows[p];
         ev_blocks[p] = 0;
         return OAMD_OK;
@@ -277,7 +300,6 @@ struct oamd_engine {
         }
         *out = span_chunks[c] + 2 * off;
         span_used = c * kSpanChunk + off + n;
-        span_launches += n;
         return OAMD_OK;
     }
     // restart the window: every launch that may still write a slot is done
@@ -287,7 +309,6 @@ struct oamd_engine {
         for (int64_t c = 0; c * kSpanChunk < span_used; ++c)
             HIPCHK(hipMemset(span_chunks[c], 0, sizeof(unsigned long long) * 2 * kSpanChunk));
         span_used = 0;
-        span_launches = 0;
         return OAMD_OK;
     }
 
@@ -420,6 +441,13 @@ struct oamd_engine {
         for (auto& pool : ev)
             for (auto e : pool) (void)hipEventDestroy(e);
         for (auto& x : span_chunks) dfree(x);
+        if (cuts_dev) {
+            (void)hipDeviceSynchronize();  // no copy into cuts_host in flight
+            dfree(cuts_dev);
+            (void)hipHostFree(cuts_host);
+            for (auto& row : cuts_ev)
+                for (auto x : row) (void)hipEventDestroy(x);
+        }
         for (int k = 0; k < n_pipe_streams; ++k) {
             (void)hipStreamDestroy(pipe_stream[k]);
             (void)hipEventDestroy(join_ev[k]);
@@ -949,7 +977,9 @@ int oamd_engine_nn_busy(const oamd_engine* ce, float* busy_ms, int64_t* launches
             if (sp[2 * i + 1]) iv.emplace_back((float)((~sp[2 * i] - t0) * 1e-5), (float)((sp[2 * i + 1] - t0) * 1e-5));
     }
     if (busy_ms) *busy_ms = (float)interval_union(iv);
-    if (launches) *launches = e->span_launches;
+    // the launches that ran (a search reserves slots for the most launches of
+    // any group per round; groups of unequal size may leave some unused)
+    if (launches) *launches = (int64_t)iv.size();
     return OAMD_OK;
 }
 
@@ -1000,9 +1030,33 @@ static int extra_rounds(const oamd_engine* e) {
     return e->exact_interleaving && e->chain_budget > 0 ? e->chain_cuts : 0;
 }
 
-// Selecting rounds (= NN rounds) of a native grouped search: one per batch of
-// a thread plus the chain-splitting extra rounds
-static int search_rounds(const oamd_engine* e, int steps) { return steps + extra_rounds(e); }
+// Extra rounds X of the next grouped search. Fixed: chain_cuts. Adaptive: a
+// game cut c times finishes by round steps + c, so the extra rounds past the
+// most cuts any game used are empty launches, while a game that would need
+// more than X cuts only runs its last chain uncut (same results, a longer
+// round). X follows the searches' demand: the most cuts u of the search two
+// back (done by now: the previous one is still queued, so the read-back does
+// not drain the queue) -> X = u + 2, or twice the X that u saturated.
+static int pick_extra_rounds(oamd_engine* e, int* X) {
+    *X = extra_rounds(e);
+    if (*X == 0 || e->adapt_min <= 0) return OAMD_OK;
+    if (int rc = e->ensure_cut_slots()) return rc;
+    const int64_t q = e->adapt_seq - 2;
+    const int s = q >= 0 ? (int)(q % oamd_engine::kCutSlots) : 0;
+    if (q >= 0 && e->cut_x[s] > 0) {
+        int used = 0;
+        for (int k = 0; k < e->cut_groups[s]; ++k) {
+            HIPCHK(hipEventSynchronize(e->cuts_ev[s][k]));
+            used = std::max(used, (int)e->cuts_host[s * kMaxPipeline + k]);
+        }
+        static const int pa = getenv("OAMD_ADAPT_A") ? atoi(getenv("OAMD_ADAPT_A")) : 1;
+        static const int pb = getenv("OAMD_ADAPT_B") ? atoi(getenv("OAMD_ADAPT_B")) : 2;
+        e->adapt_x = used >= e->cut_x[s] ? 2 * e->cut_x[s] : pa * used + pb;
+        e->cut_x[s] = 0;
+    }
+    if (e->adapt_x > 0) *X = std::clamp(e->adapt_x, std::min(e->adapt_min, *X), *X);
+    return OAMD_OK;
+}
 
 // ResNet launches per group and round (the most of any group: nn_batch splits
 // a group's rows into consecutive launches)
@@ -1017,7 +1071,7 @@ static int launches_per_group_round(const oamd_engine* e, const GroupPlan& P) {
 
 // Sampled timing of one search: claim the current event pool (every
 // timing_stride-th search), sized for NB blocks per round and `steps` NN
-// rounds (search_rounds) plus the final backup-only round.
+// rounds (steps + extra rounds) plus the final backup-only round.
 static int timing_begin(oamd_engine* e, int steps, int NB, bool* timed) {
     *timed = e->timing && (e->search_count++ % e->timing_stride) == 0;
     if (!*timed) return OAMD_OK;
@@ -1058,24 +1112,34 @@ static void timing_end(oamd_engine* e, int steps, int NB, bool split, const Grou
 // streams carry on from a previous search of the same call (a multi-move
 // self-play call), so its first NN launch also waits for the NN token.
 
-static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPlan& P, int steps, bool timed,
+static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPlan& P, int steps, int X, bool timed,
                                 bool chained) {
     const EngineView E = e->view();
     const int K = P.K, L = e->L();
     const int T = e->cfg.num_threads, B = e->cfg.batch_size;
     const int pool = e->ev_cur;
     const int nch = e->nn_chains < K ? e->nn_chains : K;
-    // chain splitting (k_tree): X extra rounds absorb the rounds a split chain
-    // delays its game by; only the reference's interleaving has chains
-    const int X = extra_rounds(e);
+    // chain splitting (k_tree): X extra rounds (pick_extra_rounds) absorb the
+    // rounds a split chain delays its game by; only the reference's
+    // interleaving has chains
     const int budget = X > 0 ? e->chain_budget : 0;
     const int S = steps + X;
+    // adaptive X: each group's most cuts, into this search's slot
+    const bool adapt = X > 0 && e->adapt_min > 0;
+    const int cs = (int)(e->adapt_seq % oamd_engine::kCutSlots);
+    ++e->grouped_searches;
+    e->grouped_rounds += S;
+    if (adapt) {
+        e->cut_x[cs] = X;
+        e->cut_groups[cs] = K;
+        ++e->adapt_seq;
+    }
     // rounds 0..S (k_tree): round s backs up what the previous rounds selected
     // and selects, thread by thread; the NN evaluates round s's selections
     // between rounds s and s+1; the last round only backs up. A timed search
     // records events for every round, the extra ones included, and counts the
     // NN rows of every round (counters [4..5]): launches, rows and busy time
-    // of a timed search cover the same launches (search_rounds)
+    // of a timed search cover the same launches (steps + X)
     const int nlg = launches_per_group_round(e, P);
     unsigned long long* span = nullptr;  // this search's busy-time slots (timing on)
     if (int rc = e->reserve_spans((int64_t)K * S * nlg, &span)) return rc;
@@ -1089,10 +1153,19 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
             // the other one (which round s-1's launch, done by now, read); the
             // final round zeroes counter 0 for the next search's round 0
             int* cnt = e->rowcount + 2 * k;
+            int* cuts = adapt ? e->cuts_dev + cs * kMaxPipeline + k : nullptr;
             launch_tree(E, sk, s > 0, s < S, T, B, P.g0[k], P.ng[k], 0, -1, s < S ? cnt + (s & 1) : nullptr,
-                        s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X, timed);
+                        s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X, timed,
+                        s == 0 || s == S ? cuts : nullptr);
             if (ev) HIPCHK(hipEventRecord(ev[1], sk));
-            if (s == S) continue;
+            if (s == S) {
+                if (adapt) {
+                    HIPCHK(hipMemcpyAsync(e->cuts_host + cs * kMaxPipeline + k, cuts, sizeof(int32_t),
+                                          hipMemcpyDeviceToHost, sk));
+                    HIPCHK(hipEventRecord(e->cuts_ev[cs][k], sk));
+                }
+                continue;
+            }
             // the groups' NN launches run one after another (OAMD_NN_ORDER)
             hipStream_t ns = sk;
             if (K > 1 && OAMD_NN_ORDER == 2) {
@@ -1167,7 +1240,9 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     // sampled timing: per (round, group) kEvPerBlock events: tree begin/end, NN
     // begin/end (on the NN stream, after its waits; not in the final round)
     bool timed = false;
-    const int rounds = split ? steps : search_rounds(e, steps);  // NN rounds
+    int X = 0;
+    if (!split && (rc = pick_extra_rounds(e, &X))) return rc;
+    const int rounds = steps + X;  // NN rounds
     if ((rc = timing_begin(e, rounds, NB, &timed))) return rc;
     const int pool = e->ev_cur;
     unsigned long long* span = nullptr;  // busy-time slots [thread][round] of the split schedule
@@ -1193,7 +1268,7 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     }
     if (!split) {
         if ((rc = fork_groups(e, P))) return rc;
-        if ((rc = enqueue_group_rounds(e, N, P, steps, timed, false))) return rc;
+        if ((rc = enqueue_group_rounds(e, N, P, steps, X, timed, false))) return rc;
     }
     LAUNCHCHK();
     if (!split && (rc = join_groups(e, P))) return rc;
@@ -1253,6 +1328,23 @@ int oamd_engine_set_chain_split(oamd_engine* e, int32_t budget, int32_t cuts) {
     if (budget < 0 || cuts < 0 || cuts > 64) return fail(OAMD_INVALID_ARGUMENT, "chain split: budget >= 0, cuts in [0, 64]");
     e->chain_budget = budget;
     e->chain_cuts = cuts;
+    return OAMD_OK;
+}
+
+int oamd_engine_set_adaptive_extra_rounds(oamd_engine* e, int32_t min_rounds) {
+    if (min_rounds < 0 || min_rounds > 64) return fail(OAMD_INVALID_ARGUMENT, "adaptive extra rounds: min in [0, 64]");
+    e->adapt_min = min_rounds;
+    e->adapt_x = 0;  // the next searches start from chain_cuts again
+    for (int& x : e->cut_x) x = 0;
+    return OAMD_OK;
+}
+
+int oamd_engine_round_counts(const oamd_engine* ce, int64_t* searches, int64_t* rounds, int64_t* final_launches) {
+    oamd_engine* e = const_cast<oamd_engine*>(ce);  // pending events are summed here
+    if (int rc = e->resolve_all_timing()) return rc;
+    if (searches) *searches = e->grouped_searches;
+    if (rounds) *rounds = e->grouped_rounds;
+    if (final_launches) *final_launches = e->tree_final_launches;
     return OAMD_OK;
 }
 
@@ -1413,12 +1505,14 @@ int oamd_engine_selfplay_steps(oamd_engine* e, oamd_net* net, const oamd_selfpla
     int rc = fork_groups(e, P);
     for (int i = 0; !rc && i < n_moves; ++i) {
         bool timed = false;
-        if ((rc = timing_begin(e, search_rounds(e, steps), P.K, &timed))) break;
-        if ((rc = enqueue_group_rounds(e, N, P, steps, timed, i > 0))) break;
+        int X = 0;
+        if ((rc = pick_extra_rounds(e, &X))) break;
+        if ((rc = timing_begin(e, steps + X, P.K, &timed))) break;
+        if ((rc = enqueue_group_rounds(e, N, P, steps, X, timed, i > 0))) break;
         for (int k = 0; k < P.K; ++k)
             launch_selfplay_move(E, sp, P.g0[k], P.ng[k], out(i, actions_dev, 1), out(i, finished_dev, 1),
                                  out(i, features_dev, 8 * C * 64), out(i, policy_dev, 8 * 65), P.st[k]);
-        if (timed) timing_end(e, search_rounds(e, steps), P.K, false, P);
+        if (timed) timing_end(e, steps + X, P.K, false, P);
     }
     if (rc) return rc;
     LAUNCHCHK();

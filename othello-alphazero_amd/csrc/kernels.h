@@ -28,7 +28,7 @@ struct SelfplayParams {
 void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
                  int g0 = 0, int ng = -1, int t0 = 0, int t1 = -1, int* cnt_add = nullptr,
                  int* cnt_reset = nullptr, bool fresh = false, int budget = 0, int max_cuts = 0,
-                 bool timed = false);
+                 bool timed = false, int* cuts_out = nullptr);
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s);
 void launch_set_evaluation(const EngineView& E, const float* pol, const float* val, int row_begin,
                            int rows, hipStream_t s);

@@ -670,6 +670,13 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
              [](Engine& e, int workgroups) { check(oamd_engine_set_extra_round_grid(e.h, workgroups)); })
         .def("set_chain_split",
              [](Engine& e, int budget, int cuts) { check(oamd_engine_set_chain_split(e.h, budget, cuts)); })
+        .def("set_adaptive_extra_rounds",
+             [](Engine& e, int min_rounds) { check(oamd_engine_set_adaptive_extra_rounds(e.h, min_rounds)); })
+        .def("round_counts", [](Engine& e) {
+            int64_t searches = 0, rounds = 0, finals = 0;
+            check(oamd_engine_round_counts(e.h, &searches, &rounds, &finals));
+            return py::make_tuple(searches, rounds, finals);
+        })
         .def("set_exact_interleaving",
              [](Engine& e, bool enable) { check(oamd_engine_set_exact_interleaving(e.h, enable ? 1 : 0)); })
         .def("nn_timing", [](Engine& e) {

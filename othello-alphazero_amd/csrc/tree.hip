@@ -532,10 +532,14 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
 // rounds always start at thread 0 (the step API and the single-game split).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree(EngineView E, int g0, int do_backup, int do_select,
                                              int t0, int t1, int B, int* cnt_add, int* cnt_reset, int fresh,
-                                             int budget, int max_cuts, int timed) {
+                                             int budget, int max_cuts, int timed, int* cuts_out) {
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
+    // cuts_out: the most cuts any game of the launch's groups used in this
+    // search (adaptive extra rounds, capi.hip): zeroed by the search's first
+    // round, raised by its final (backup-only) round
+    if (cuts_out && fresh && blockIdx.x == 0 && lane == 0) *cuts_out = 0;
 #ifdef OAMD_TREE_STAMPS
     if (lane < kTsCount) ts_acc[lane] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -625,6 +629,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
             gs->resume = cut_at >= 0 ? cut_at : rp;
             gs->cuts = cuts;
         }
+        if (cuts_out && !do_select) atomicMax(cuts_out, cuts);
         gs->event = event;
         gs->count = count;
         // atomic like select_range's kDepthCap: a plain read-modify-write of
@@ -1053,13 +1058,14 @@ static inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b -
 
 void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_select, int T, int B,
                  int g0, int ng, int t0, int t1, int* cnt_add, int* cnt_reset, bool fresh, int budget,
-                 int max_cuts, bool timed) {
+                 int max_cuts, bool timed, int* cuts_out) {
     if (ng < 0) ng = E.G - g0;
     if (t1 < 0) t1 = T;
     if (T * B != E.L || t0 < 0 || t1 > T || t0 >= t1) return;  // caller validated; never launch on a mismatched layout
     if (ng > 0 && (do_backup || do_select))
         hipLaunchKernelGGL(k_tree, dim3(ng), dim3(64), 0, s, E, g0, (int)do_backup, (int)do_select, t0, t1, B,
-                           do_select ? cnt_add : nullptr, cnt_reset, (int)fresh, budget, max_cuts, (int)timed);
+                           do_select ? cnt_add : nullptr, cnt_reset, (int)fresh, budget, max_cuts, (int)timed,
+                           cuts_out);
 }
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s) {
     if (rows > 0) hipLaunchKernelGGL(k_features_f32, dim3(blocks_for(rows, 4)), dim3(256), 0, s, E, out, row_begin, rows);

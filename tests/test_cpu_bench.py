@@ -21,7 +21,8 @@ def _m(launches=66, busy_per=0.75, span_per=1.05, rows=4096, evals_share=0.9, st
     # the window (steps searches)
     return {"nn_ms": span_per * launches, "nn_busy_ms": busy_per * launches * steps, "nn_launches": launches,
             "busy_launches": launches * steps, "nn_rows": rows * launches,
-            "select_ms": 0.45 * 33 * 2, "backup_ms": 0.13 * 2, "tree_launches": 33 * 2,
+            "select_ms": 0.45 * 33 * 2, "backup_ms": 0.13 * 2, "tree_launches": 33 * 2, "final_launches": 2,
+            "searches": steps, "rounds": 33 * steps,
             "sims": 256 * 800 * steps, "evals": int(256 * 800 * steps * evals_share), "overflow_games": 0}
 
 
@@ -44,6 +45,7 @@ def test_roofline_uses_union_busy_time_and_timed_rows():
     t = out["tree_kernels"]
     assert t["k_tree"]["avg_launch_ms"] == pytest.approx(0.45)
     assert t["k_tree_final_backup"]["avg_launch_ms"] == pytest.approx(0.13)
+    assert t["rounds_per_search"] == 33 and t["max_rounds_per_search"] == 41
 
 
 def test_one_chain_union_equals_summed_durations():
@@ -52,27 +54,33 @@ def test_one_chain_union_equals_summed_durations():
     assert r["avg_launch_ms"] == r["busy_ms_per_launch"] and r["nn_chains"] == 1
 
 
-def test_rounds_and_timed_region_launches():
-    """Every round of a search is an NN round: 25 batches per thread + the
-    chain-splitting extra rounds (exact interleaving only); the timed region's
-    k_resnet dispatches are steps x groups x rounds x launches per group."""
+def test_rounds_per_search():
+    """Every round of a search is an NN round: 25 batches per thread + up to
+    chain_cuts extra rounds (exact interleaving only; the engine's adaptive
+    count, reported as searches and rounds: the record carries the average);
+    the timed region's k_resnet dispatches are the launches the engine saw."""
     a = bench.parse_args([])
-    assert bench.search_rounds(a) == 33 and bench.pipeline_groups(a) == 2
-    assert bench.timed_region_resnet_launches(a) == 10 * 2 * 33
+    assert bench.max_search_rounds(a) == 41 and bench.pipeline_groups(a) == 2
     a = bench.parse_args(["--round-robin-endgames"])
-    assert bench.search_rounds(a) == 25
-    a = bench.parse_args(["--chain-budget", "0", "--steps", "4"])
-    assert bench.timed_region_resnet_launches(a) == 4 * 2 * 25
-    # configs[4] shard: 2048-row launches over 512 games (2 x 8192-row groups)
-    a = bench.parse_args(["--games", "512", "--dtype", "fp16", "--eval-batch", "2048", "--steps", "3"])
-    assert bench.timed_region_resnet_launches(a) == 3 * 33 * 2 * 4
+    assert bench.max_search_rounds(a) == 25
+    a = bench.parse_args(["--chain-budget", "0"])
+    assert bench.max_search_rounds(a) == 25
     # configs[3]: 1600 sims = 50 batches per thread
     a = bench.parse_args(["--sims", "1600", "--channels", "256", "--blocks", "20"])
-    assert bench.search_rounds(a) == 58
+    assert bench.max_search_rounds(a) == 66
     # one game, T > 1: the thread-split schedule has no extra rounds
     a = bench.parse_args(["--games", "1"])
-    assert bench.single_game_split(a) and bench.search_rounds(a) == 25
-    assert bench.timed_region_resnet_launches(a) == 10 * 25 * 2
+    assert bench.single_game_split(a) and bench.max_search_rounds(a) == 25
+    # 10 searches averaging 28.5 rounds (25 + adaptive 3.5)
+    m = _m()
+    m.update(searches=10, rounds=285, busy_launches=570)
+    out = bench.measured_fields(bench.parse_args([]), m, "w")
+    assert out["tree_kernels"]["rounds_per_search"] == 28.5
+    assert out["roofline"]["timed_region_launches"] == 570 == out["roofline"]["launches"]
+    # no grouped search (the single-game split): the fixed count
+    m.update(searches=0, rounds=0)
+    out = bench.measured_fields(bench.parse_args(["--games", "1"]), m, "w")
+    assert out["tree_kernels"]["rounds_per_search"] == 25
 
 
 def test_n_eval_per_launch_within_launched_rows_with_extra_rounds():
@@ -150,8 +158,7 @@ def test_sustained_record_uses_its_own_moves():
     """The `sustained` sub-record (moves after the timed region): its rate,
     rows launched and timed-region launches count its own moves."""
     args = bench.parse_args(["--steps", "10", "--sustained-moves", "64"])
-    m = _m()
-    m["sims"] = 256 * 800 * 64
+    m = _m(steps=64)
     m["evals"] = int(m["sims"] * 0.85)
     out = bench.sustained_fields(args, m, 1, 800, 2.56)
     assert out["moves"] == 64 and out["value"] == pytest.approx(256 * 800 * 64 / 2.56, rel=1e-6)

@@ -299,14 +299,16 @@ def test_chain_split_keeps_every_game_identical(om):
     net = om.NativeNet(alphazero_state_dict(43, 9, 128, 1, 32), device=0)
     kw = dict(history_size=4, num_simulations=320, num_threads=2, batch_size=16, dirichlet_epsilon=0.25, seed=8,
               node_capacity=1 << 17)
-    # (budget, cuts, extra-round grid): the extra rounds' ResNet launches loop
-    # over the lagging games' rows on a small grid (1 workgroup: every board
-    # group in turn) or use the regular grid (0)
-    splits = [(0, 0, 128), (1, 3, 128), (4, 4, 128), (4, 8, 1), (1, 8, 0)]
+    # (budget, cuts, extra-round grid, adaptive minimum): the extra rounds'
+    # ResNet launches loop over the lagging games' rows on a small grid (1
+    # workgroup: every board group in turn) or use the regular grid (0); the
+    # extra-round count X adapts per search (minimum 1 or 2) or stays at cuts (0)
+    splits = [(0, 0, 128, 2), (1, 3, 128, 2), (4, 4, 128, 0), (4, 8, 1, 2), (1, 8, 0, 0), (1, 16, 128, 1)]
     engines = [om.BatchedMCTS(64, **kw) for _ in splits]
-    for x, (budget, cuts, grid) in zip(engines, splits):
+    for x, (budget, cuts, grid, amin) in zip(engines, splits):
         x.engine.set_chain_split(budget, cuts)
         x.engine.set_extra_round_grid(grid)
+        x.engine.set_adaptive_extra_rounds(amin)
     ref = om.BatchedMCTS(64, **kw)
     for x in engines + [ref]:
         x.random_openings(50, seed=9)
@@ -324,8 +326,15 @@ def test_chain_split_keeps_every_game_identical(om):
             o = x.selfplay_move(temperature_moves=12, opening_moves=50)
             assert torch.equal(o["actions"], xr["actions"]) and torch.equal(o["finished"], xr["finished"]), (mv, sp)
     share = 1.0 - total_evals / total_sims
+    # the adaptive count ran fewer extra rounds than the fixed one would have
+    # (10 batches per thread and search), the fixed count exactly cuts
+    rounds = {sp: x.engine.round_counts() for x, sp in zip(engines, splits)}
+    assert rounds[(4, 4, 128, 0)][:2] == (24, 24 * 14) and rounds[(1, 8, 0, 0)][:2] == (24, 24 * 18)
+    n, r, _ = rounds[(1, 16, 128, 1)]
+    assert n == 24 and 24 * 11 <= r < 24 * 26
     numerics.record("chain split", f"64 late games x 24 moves: terminal-leaf share {share:.3f}, "
-                                   "budgets 0/1/4, extra-round grids 1/128/regular == callback")
+                                   "budgets 0/1/4, extra-round grids 1/128/regular, fixed and adaptive extra "
+                                   f"rounds (budget 1, <= 16 cuts: {r / n - 10:.2f} per search) == callback")
     assert share > 0.1
 
 
