@@ -180,16 +180,22 @@ struct oamd_engine {
     static constexpr int kCutSlots = 4;
     int adapt_min = 2;
     int adapt_x = 0;         // the last X picked from a measurement (0: none yet)
+    // endgame threshold: at most this many empty squares on some game's root
+    // (two moves before the search) -> X = chain_cuts; raised past every root
+    // whose search needed cuts
+    static constexpr int kEndgameEmpties = 12;
+    int adapt_empties = kEndgameEmpties;
     int64_t adapt_seq = 0;   // grouped searches enqueued with a cuts slot
-    int32_t* cuts_dev = nullptr;   // [kCutSlots][kMaxPipeline] most cuts per search and group
+    // [kCutSlots][kMaxPipeline][2] per search and group: most cuts, fewest root empties
+    int32_t* cuts_dev = nullptr;
     int32_t* cuts_host = nullptr;  // pinned copies
     int cut_x[kCutSlots] = {};     // X of the search in the slot (0: slot empty)
     int cut_groups[kCutSlots] = {};
     hipEvent_t cuts_ev[kCutSlots][kMaxPipeline] = {};
     int ensure_cut_slots() {
         if (cuts_dev) return OAMD_OK;
-        if (int rc = dalloc(&cuts_dev, (size_t)kCutSlots * kMaxPipeline)) return rc;
-        HIPCHK(hipHostMalloc((void**)&cuts_host, sizeof(int32_t) * kCutSlots * kMaxPipeline));
+        if (int rc = dalloc(&cuts_dev, (size_t)2 * kCutSlots * kMaxPipeline)) return rc;
+        HIPCHK(hipHostMalloc((void**)&cuts_host, sizeof(int32_t) * 2 * kCutSlots * kMaxPipeline));
         for (auto& row : cuts_ev)
             for (auto& x : row) HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
         return OAMD_OK;
@@ -1033,10 +1039,10 @@ static int extra_rounds(const oamd_engine* e) {
 // Extra rounds X of the next grouped search. Fixed: chain_cuts. Adaptive: a
 // game cut c times finishes by round steps + c, so the extra rounds past the
 // most cuts any game used are empty launches, while a game that would need
-// more than X cuts only runs its last chain uncut (same results, a longer
-// round). X follows the searches' demand: the most cuts u of the search two
-// back (done by now: the previous one is still queued, so the read-back does
-// not drain the queue) -> X = u + 2, or twice the X that u saturated.
+// more than X cuts runs its last chain uncut (same results, but a round of up
+// to ~10 ms that holds its group's NN launch). X follows the search two back
+// (done by now: the previous one is still queued, so the read-back does not
+// drain the queue): its most cuts and the fewest empty squares of its roots.
 static int pick_extra_rounds(oamd_engine* e, int* X) {
     *X = extra_rounds(e);
     if (*X == 0 || e->adapt_min <= 0) return OAMD_OK;
@@ -1044,14 +1050,26 @@ static int pick_extra_rounds(oamd_engine* e, int* X) {
     const int64_t q = e->adapt_seq - 2;
     const int s = q >= 0 ? (int)(q % oamd_engine::kCutSlots) : 0;
     if (q >= 0 && e->cut_x[s] > 0) {
-        int used = 0;
+        int used = 0, empties = 64;
         for (int k = 0; k < e->cut_groups[s]; ++k) {
             HIPCHK(hipEventSynchronize(e->cuts_ev[s][k]));
-            used = std::max(used, (int)e->cuts_host[s * kMaxPipeline + k]);
+            used = std::max(used, (int)e->cuts_host[2 * (s * kMaxPipeline + k)]);
+            empties = std::min(empties, (int)e->cuts_host[2 * (s * kMaxPipeline + k) + 1]);
         }
-        static const int pa = getenv("OAMD_ADAPT_A") ? atoi(getenv("OAMD_ADAPT_A")) : 1;
-        static const int pb = getenv("OAMD_ADAPT_B") ? atoi(getenv("OAMD_ADAPT_B")) : 2;
-        e->adapt_x = used >= e->cut_x[s] ? 2 * e->cut_x[s] : pa * used + pb;
+        // the cuts come with the endgame: outside it no chain outlasts the
+        // budget (used = 0), within ~9 empty squares of the end a game's whole
+        // search can be all terminal (used = 12 of 50 batches per thread at
+        // budget 4; profiles/r04/ab/adaptive_demand_log.txt). The root loses
+        // one empty square per move, so the fewest empties two searches back
+        // announce the endgame before it starts; a search that needed cuts
+        // raises the threshold past its root. Outside the endgame X = the
+        // cuts used + 2 (2X if they were all used)
+        if (used > 0) e->adapt_empties = std::max(e->adapt_empties, empties + 3);
+        if (empties <= e->adapt_empties) e->adapt_x = e->chain_cuts;
+        else e->adapt_x = (used >= e->cut_x[s] ? 2 * e->cut_x[s] : used) + 2;
+        static const bool plog = getenv("OAMD_ADAPT_LOG") != nullptr;
+        if (plog)
+            fprintf(stderr, "adapt search %lld X %d used %d empties %d\n", (long long)q, e->cut_x[s], used, empties);
         e->cut_x[s] = 0;
     }
     if (e->adapt_x > 0) *X = std::clamp(e->adapt_x, std::min(e->adapt_min, *X), *X);
@@ -1153,14 +1171,14 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
             // the other one (which round s-1's launch, done by now, read); the
             // final round zeroes counter 0 for the next search's round 0
             int* cnt = e->rowcount + 2 * k;
-            int* cuts = adapt ? e->cuts_dev + cs * kMaxPipeline + k : nullptr;
+            int* cuts = adapt ? e->cuts_dev + 2 * (cs * kMaxPipeline + k) : nullptr;
             launch_tree(E, sk, s > 0, s < S, T, B, P.g0[k], P.ng[k], 0, -1, s < S ? cnt + (s & 1) : nullptr,
                         s < S ? cnt + ((s + 1) & 1) : cnt, s == 0, budget, X, timed,
                         s == 0 || s == S ? cuts : nullptr);
             if (ev) HIPCHK(hipEventRecord(ev[1], sk));
             if (s == S) {
                 if (adapt) {
-                    HIPCHK(hipMemcpyAsync(e->cuts_host + cs * kMaxPipeline + k, cuts, sizeof(int32_t),
+                    HIPCHK(hipMemcpyAsync(e->cuts_host + 2 * (cs * kMaxPipeline + k), cuts, 2 * sizeof(int32_t),
                                           hipMemcpyDeviceToHost, sk));
                     HIPCHK(hipEventRecord(e->cuts_ev[cs][k], sk));
                 }
@@ -1335,6 +1353,7 @@ int oamd_engine_set_adaptive_extra_rounds(oamd_engine* e, int32_t min_rounds) {
     if (min_rounds < 0 || min_rounds > 64) return fail(OAMD_INVALID_ARGUMENT, "adaptive extra rounds: min in [0, 64]");
     e->adapt_min = min_rounds;
     e->adapt_x = 0;  // the next searches start from chain_cuts again
+    e->adapt_empties = oamd_engine::kEndgameEmpties;
     for (int& x : e->cut_x) x = 0;
     return OAMD_OK;
 }

@@ -536,10 +536,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
-    // cuts_out: the most cuts any game of the launch's groups used in this
-    // search (adaptive extra rounds, capi.hip): zeroed by the search's first
-    // round, raised by its final (backup-only) round
-    if (cuts_out && fresh && blockIdx.x == 0 && lane == 0) *cuts_out = 0;
+    // cuts_out (adaptive extra rounds, capi.hip): [0] the most cuts any game
+    // of the launch's group used in this search, [1] the fewest empty squares
+    // of an active game's root; reset by the search's first round, set by its
+    // final (backup-only) round
+    if (cuts_out && fresh && blockIdx.x == 0 && lane == 0) {
+        cuts_out[0] = 0;
+        cuts_out[1] = 64;
+    }
 #ifdef OAMD_TREE_STAMPS
     if (lane < kTsCount) ts_acc[lane] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -629,7 +633,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
             gs->resume = cut_at >= 0 ? cut_at : rp;
             gs->cuts = cuts;
         }
-        if (cuts_out && !do_select) atomicMax(cuts_out, cuts);
+        if (cuts_out && !do_select) {
+            const NodePos& rp = E.pos[base + gs->root];
+            atomicMax(cuts_out, cuts);
+            atomicMin(cuts_out + 1, 64 - __popcll(rp.p1 | rp.p2));
+        }
         gs->event = event;
         gs->count = count;
         // atomic like select_range's kDepthCap: a plain read-modify-write of

@@ -326,16 +326,49 @@ def test_chain_split_keeps_every_game_identical(om):
             o = x.selfplay_move(temperature_moves=12, opening_moves=50)
             assert torch.equal(o["actions"], xr["actions"]) and torch.equal(o["finished"], xr["finished"]), (mv, sp)
     share = 1.0 - total_evals / total_sims
-    # the adaptive count ran fewer extra rounds than the fixed one would have
-    # (10 batches per thread and search), the fixed count exactly cuts
+    # the fixed count runs exactly cuts extra rounds (10 batches per thread
+    # and search); these late games are in the adaptive count's endgame
     rounds = {sp: x.engine.round_counts() for x, sp in zip(engines, splits)}
     assert rounds[(4, 4, 128, 0)][:2] == (24, 24 * 14) and rounds[(1, 8, 0, 0)][:2] == (24, 24 * 18)
     n, r, _ = rounds[(1, 16, 128, 1)]
-    assert n == 24 and 24 * 11 <= r < 24 * 26
+    assert n == 24 and 24 * 11 <= r <= 24 * 26
     numerics.record("chain split", f"64 late games x 24 moves: terminal-leaf share {share:.3f}, "
                                    "budgets 0/1/4, extra-round grids 1/128/regular, fixed and adaptive extra "
                                    f"rounds (budget 1, <= 16 cuts: {r / n - 10:.2f} per search) == callback")
     assert share > 0.1
+
+
+@pytest.mark.parametrize("opening", [4, 50])
+def test_adaptive_extra_rounds(om, opening):
+    """The adaptive extra-round count (capi.hip pick_extra_rounds): the first
+    two searches run chain_cuts extra rounds; from the third on, early games
+    (4-ply openings: no terminal leaf, no cut) run the minimum, games within
+    12 empty squares of the end (openings of 0-50 plies over 256 games: some
+    game is) the full count. Through
+    the multi-move self-play call (one pipeline group per stream), the moves
+    equal those of the fixed count."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(46, 9, 128, 1, 32), device=0)
+    kw = dict(history_size=4, num_simulations=320, num_threads=2, batch_size=16, dirichlet_epsilon=0.25, seed=12,
+              node_capacity=1 << 17)
+    runs = []
+    for amin in (2, 0):
+        x = om.BatchedMCTS(256, **kw)
+        x.engine.set_chain_split(4, 16)
+        x.engine.set_adaptive_extra_rounds(amin)
+        x.random_openings(opening, seed=13)
+        out = x.selfplay_steps(net, 6, temperature_moves=12, opening_moves=opening, emit_targets=True)
+        torch.cuda.synchronize()
+        runs.append((x.engine.round_counts(), out))
+    (n, r, _), out = runs[0]
+    (nf, rf, _), out_f = runs[1]
+    assert n == nf == 6 and rf == 6 * 26
+    assert r == (2 * 26 + 4 * 12 if opening == 4 else 6 * 26), (opening, r)
+    for k in out:
+        assert torch.equal(out[k], out_f[k]), k
+    numerics.record(f"adaptive extra rounds, {opening}-ply openings", f"{r - 60} extra rounds in 6 searches "
+                    f"(fixed: {rf - 60}); moves and targets identical")
 
 
 def test_chain_split_with_more_than_64_threads(om):
