@@ -327,8 +327,10 @@ def parse_args(argv: list[str]):
                          "(0 = never split; exact interleaving only)")
     ap.add_argument("--chain-cuts", type=int, default=16,
                     help="most chain splits per game and search (= most extra rounds)")
-    ap.add_argument("--adaptive-min", type=int, default=2,
-                    help="fewest extra rounds of the adaptive count (0 = always --chain-cuts)")
+    ap.add_argument("--adaptive-min", type=int, default=1,
+                    help="fewest extra rounds of the adaptive count (the margin over the cuts used)")
+    ap.add_argument("--fixed-extra-rounds", action="store_true",
+                    help="always --chain-cuts extra rounds (no adaptive count)")
     ap.add_argument("--extra-grid", type=int, default=128,
                     help="workgroups of the extra rounds' ResNet launches (0 = the regular grid)")
     ap.add_argument("--cpu-baseline-moves", type=int, default=24,
@@ -428,7 +430,7 @@ class EngineWorkload:
         self.b.engine.set_exact_interleaving(not args.round_robin_endgames)
         self.b.engine.set_chain_split(args.chain_budget, args.chain_cuts)
         self.b.engine.set_extra_round_grid(args.extra_grid)
-        self.b.engine.set_adaptive_extra_rounds(args.adaptive_min)
+        self.b.engine.set_adaptive_extra_rounds(not args.fixed_extra_rounds, args.adaptive_min)
         props = torch.cuda.get_device_properties(local)
         self.device_id = f"{os.uname().nodename}:{getattr(props, 'uuid', local)}"
 
@@ -543,7 +545,7 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
                                      f"exact (reference), chains split after {args.chain_budget} re-selections, "
                                      f"<= X times per search, X extra rounds, X adaptive in "
                                      f"[{min(args.adaptive_min, args.chain_cuts)}, {args.chain_cuts}]"
-                                     if args.adaptive_min > 0 else
+                                     if not args.fixed_extra_rounds else
                                      f"<= {args.chain_cuts} times per search"),
             "calls": ("search + selfplay_move per step" if args.per_move_calls or args.sync_search
                       else f"one selfplay_steps call for the {args.steps} timed steps"),

@@ -188,14 +188,16 @@ int oamd_engine_set_nn_chains(oamd_engine *e, int32_t chains);
  * Default budget 4, cuts 16; budget 0 = never split. Results do not depend on
  * it. */
 int oamd_engine_set_chain_split(oamd_engine *e, int32_t budget, int32_t cuts);
-/* Adaptive extra rounds (default min_rounds 2): a grouped native search runs
- * X extra rounds and allows X cuts per game, X in [min(min_rounds, cuts),
- * cuts], following the most cuts u any game used two searches earlier (X =
- * u + 2, or twice that search's X when u reached it; read back without
- * draining the queue). Extra rounds past every game's last cut are empty
+/* Adaptive extra rounds (default on, min_rounds 1): a grouped native search
+ * runs X extra rounds and allows X cuts per game, X in [min(min_rounds,
+ * cuts), cuts], following the search two back (read back without draining
+ * the queue): X = cuts when some root of that search was within 12 empty
+ * squares of the end (the endgame, where all-terminal chains appear), else
+ * the most cuts u any game used + min_rounds (2X + 2 + min_rounds when a
+ * game ran out of cuts). Extra rounds past every game's last cut are empty
  * launches; a game that would need more cuts runs its last chain uncut.
- * min_rounds = 0: X = cuts always. Scheduling only: results are identical. */
-int oamd_engine_set_adaptive_extra_rounds(oamd_engine *e, int32_t min_rounds);
+ * enable = 0: X = cuts always. Scheduling only: results are identical. */
+int oamd_engine_set_adaptive_extra_rounds(oamd_engine *e, int32_t enable, int32_t min_rounds);
 /* Counts since the engine was created: grouped native searches enqueued (all
  * pipeline groups of one search count once), their NN rounds (steps + extra
  * rounds each), and the final backup-only k_tree launches of the timed

@@ -175,11 +175,12 @@ struct oamd_engine {
     int chain_cuts = 16;
     // adaptive extra rounds (pick_extra_rounds): a grouped search runs X in
     // [min(adapt_min, chain_cuts), chain_cuts] extra rounds (and allows X
-    // cuts), X following the most cuts any game used two searches earlier.
-    // adapt_min = 0: always chain_cuts
+    // cuts), X following the search two back. adapt_on = false: always
+    // chain_cuts
     static constexpr int kCutSlots = 4;
-    int adapt_min = 2;
-    int adapt_x = 0;         // the last X picked from a measurement (0: none yet)
+    bool adapt_on = true;
+    int adapt_min = 1;
+    int adapt_x = -1;        // the last X picked from a measurement (-1: none yet)
     // endgame threshold: at most this many empty squares on some game's root
     // (two moves before the search) -> X = chain_cuts; raised past every root
     // whose search needed cuts
@@ -189,7 +190,7 @@ struct oamd_engine {
     // [kCutSlots][kMaxPipeline][2] per search and group: most cuts, fewest root empties
     int32_t* cuts_dev = nullptr;
     int32_t* cuts_host = nullptr;  // pinned copies
-    int cut_x[kCutSlots] = {};     // X of the search in the slot (0: slot empty)
+    int cut_x[kCutSlots] = {-1, -1, -1, -1};  // X of the search in the slot (-1: slot empty)
     int cut_groups[kCutSlots] = {};
     hipEvent_t cuts_ev[kCutSlots][kMaxPipeline] = {};
     int ensure_cut_slots() {
@@ -1045,11 +1046,11 @@ static int extra_rounds(const oamd_engine* e) {
 // drain the queue): its most cuts and the fewest empty squares of its roots.
 static int pick_extra_rounds(oamd_engine* e, int* X) {
     *X = extra_rounds(e);
-    if (*X == 0 || e->adapt_min <= 0) return OAMD_OK;
+    if (*X == 0 || !e->adapt_on) return OAMD_OK;
     if (int rc = e->ensure_cut_slots()) return rc;
     const int64_t q = e->adapt_seq - 2;
     const int s = q >= 0 ? (int)(q % oamd_engine::kCutSlots) : 0;
-    if (q >= 0 && e->cut_x[s] > 0) {
+    if (q >= 0 && e->cut_x[s] >= 0) {
         int used = 0, empties = 64;
         for (int k = 0; k < e->cut_groups[s]; ++k) {
             HIPCHK(hipEventSynchronize(e->cuts_ev[s][k]));
@@ -1063,16 +1064,18 @@ static int pick_extra_rounds(oamd_engine* e, int* X) {
         // one empty square per move, so the fewest empties two searches back
         // announce the endgame before it starts; a search that needed cuts
         // raises the threshold past its root. Outside the endgame X = the
-        // cuts used + 2 (2X if they were all used)
+        // cuts used + the minimum, or 2X + 2 when a game ran out of cuts
+        // (k_tree reports X + 1: X = 0 still counts the chains that would
+        // have been split)
         if (used > 0) e->adapt_empties = std::max(e->adapt_empties, empties + 3);
         if (empties <= e->adapt_empties) e->adapt_x = e->chain_cuts;
-        else e->adapt_x = (used >= e->cut_x[s] ? 2 * e->cut_x[s] : used) + 2;
+        else e->adapt_x = (used > e->cut_x[s] ? 2 * e->cut_x[s] + 2 : used) + e->adapt_min;
         static const bool plog = getenv("OAMD_ADAPT_LOG") != nullptr;
         if (plog)
             fprintf(stderr, "adapt search %lld X %d used %d empties %d\n", (long long)q, e->cut_x[s], used, empties);
-        e->cut_x[s] = 0;
+        e->cut_x[s] = -1;
     }
-    if (e->adapt_x > 0) *X = std::clamp(e->adapt_x, std::min(e->adapt_min, *X), *X);
+    if (e->adapt_x >= 0) *X = std::clamp(e->adapt_x, std::min(e->adapt_min, *X), *X);
     return OAMD_OK;
 }
 
@@ -1140,10 +1143,13 @@ static int enqueue_group_rounds(oamd_engine* e, const NetView& N, const GroupPla
     // chain splitting (k_tree): X extra rounds (pick_extra_rounds) absorb the
     // rounds a split chain delays its game by; only the reference's
     // interleaving has chains
-    const int budget = X > 0 ? e->chain_budget : 0;
+    // (X = 0 picked by the adaptive count keeps the budget: k_tree reports
+    // the chains it could not split)
+    const bool splitting = extra_rounds(e) > 0;
+    const int budget = splitting ? e->chain_budget : 0;
     const int S = steps + X;
     // adaptive X: each group's most cuts, into this search's slot
-    const bool adapt = X > 0 && e->adapt_min > 0;
+    const bool adapt = splitting && e->adapt_on;
     const int cs = (int)(e->adapt_seq % oamd_engine::kCutSlots);
     ++e->grouped_searches;
     e->grouped_rounds += S;
@@ -1349,12 +1355,13 @@ int oamd_engine_set_chain_split(oamd_engine* e, int32_t budget, int32_t cuts) {
     return OAMD_OK;
 }
 
-int oamd_engine_set_adaptive_extra_rounds(oamd_engine* e, int32_t min_rounds) {
+int oamd_engine_set_adaptive_extra_rounds(oamd_engine* e, int32_t enable, int32_t min_rounds) {
     if (min_rounds < 0 || min_rounds > 64) return fail(OAMD_INVALID_ARGUMENT, "adaptive extra rounds: min in [0, 64]");
+    e->adapt_on = enable != 0;
     e->adapt_min = min_rounds;
-    e->adapt_x = 0;  // the next searches start from chain_cuts again
+    e->adapt_x = -1;  // the next searches start from chain_cuts again
     e->adapt_empties = oamd_engine::kEndgameEmpties;
-    for (int& x : e->cut_x) x = 0;
+    for (int& x : e->cut_x) x = -1;
     return OAMD_OK;
 }
 

@@ -671,7 +671,10 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
         .def("set_chain_split",
              [](Engine& e, int budget, int cuts) { check(oamd_engine_set_chain_split(e.h, budget, cuts)); })
         .def("set_adaptive_extra_rounds",
-             [](Engine& e, int min_rounds) { check(oamd_engine_set_adaptive_extra_rounds(e.h, min_rounds)); })
+             [](Engine& e, bool enable, int min_rounds) {
+                 check(oamd_engine_set_adaptive_extra_rounds(e.h, enable ? 1 : 0, min_rounds));
+             },
+             py::arg("enable") = true, py::arg("min_rounds") = 1)
         .def("round_counts", [](Engine& e) {
             int64_t searches = 0, rounds = 0, finals = 0;
             check(oamd_engine_round_counts(e.h, &searches, &rounds, &finals));

@@ -576,6 +576,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     const int rp = budget > 0 && !fresh ? gs->resume : t0;  // this round's first thread
     int cuts = budget > 0 && !fresh ? gs->cuts : 0;
     int chain = 0;     // re-selections after all-terminal batches in this round
+    bool over = false;  // a chain went past the budget with every cut used
     int cut_at = -1;   // the thread whose chain this round stopped
     // a search's first round starts every thread fresh, also the ones a split
     // chain keeps it from visiting (their state is read from the next round on)
@@ -599,10 +600,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
         // then the thread selects again, up to `steps` batches per search
         bool again = false;  // the last batch was all terminal and is backed up
         while (do_select && !pend && sel < E.steps) {
-            if (again && budget > 0 && chain >= budget && cuts < max_cuts) {
-                cut_at = t;  // the next round continues this chain
-                ++cuts;
-                break;
+            if (again && budget > 0 && chain >= budget) {
+                if (cuts < max_cuts) {
+                    cut_at = t;  // the next round continues this chain
+                    ++cuts;
+                    break;
+                }
+                over = true;  // no cut left: the chain runs on in this round
             }
             const unsigned long long ev0 = evals;
             TS_T(tsel0);
@@ -631,7 +635,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     if (lane == 0) {
         if (budget > 0) {
             gs->resume = cut_at >= 0 ? cut_at : rp;
-            gs->cuts = cuts;
+            // a search that ran out of cuts reports max_cuts + 1 (cuts_out)
+            gs->cuts = over ? max_cuts + 1 : cuts;
         }
         if (cuts_out && !do_select) {
             const NodePos& rp = E.pos[base + gs->root];

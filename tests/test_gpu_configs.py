@@ -302,13 +302,14 @@ def test_chain_split_keeps_every_game_identical(om):
     # (budget, cuts, extra-round grid, adaptive minimum): the extra rounds'
     # ResNet launches loop over the lagging games' rows on a small grid (1
     # workgroup: every board group in turn) or use the regular grid (0); the
-    # extra-round count X adapts per search (minimum 1 or 2) or stays at cuts (0)
-    splits = [(0, 0, 128, 2), (1, 3, 128, 2), (4, 4, 128, 0), (4, 8, 1, 2), (1, 8, 0, 0), (1, 16, 128, 1)]
+    # extra-round count X adapts per search (minimum 0, 1 or 2) or stays at
+    # cuts (None)
+    splits = [(0, 0, 128, 0), (1, 3, 128, 2), (4, 4, 128, None), (4, 8, 1, 0), (1, 8, 0, None), (1, 16, 128, 1)]
     engines = [om.BatchedMCTS(64, **kw) for _ in splits]
     for x, (budget, cuts, grid, amin) in zip(engines, splits):
         x.engine.set_chain_split(budget, cuts)
         x.engine.set_extra_round_grid(grid)
-        x.engine.set_adaptive_extra_rounds(amin)
+        x.engine.set_adaptive_extra_rounds(amin is not None, amin or 0)
     ref = om.BatchedMCTS(64, **kw)
     for x in engines + [ref]:
         x.random_openings(50, seed=9)
@@ -329,7 +330,7 @@ def test_chain_split_keeps_every_game_identical(om):
     # the fixed count runs exactly cuts extra rounds (10 batches per thread
     # and search); these late games are in the adaptive count's endgame
     rounds = {sp: x.engine.round_counts() for x, sp in zip(engines, splits)}
-    assert rounds[(4, 4, 128, 0)][:2] == (24, 24 * 14) and rounds[(1, 8, 0, 0)][:2] == (24, 24 * 18)
+    assert rounds[(4, 4, 128, None)][:2] == (24, 24 * 14) and rounds[(1, 8, 0, None)][:2] == (24, 24 * 18)
     n, r, _ = rounds[(1, 16, 128, 1)]
     assert n == 24 and 24 * 11 <= r <= 24 * 26
     numerics.record("chain split", f"64 late games x 24 moves: terminal-leaf share {share:.3f}, "
@@ -342,7 +343,7 @@ def test_chain_split_keeps_every_game_identical(om):
 def test_adaptive_extra_rounds(om, opening):
     """The adaptive extra-round count (capi.hip pick_extra_rounds): the first
     two searches run chain_cuts extra rounds; from the third on, early games
-    (4-ply openings: no terminal leaf, no cut) run the minimum, games within
+    (4-ply openings: no terminal leaf, no cut) run none, games within
     12 empty squares of the end (openings of 0-50 plies over 256 games: some
     game is) the full count. Through
     the multi-move self-play call (one pipeline group per stream), the moves
@@ -353,10 +354,10 @@ def test_adaptive_extra_rounds(om, opening):
     kw = dict(history_size=4, num_simulations=320, num_threads=2, batch_size=16, dirichlet_epsilon=0.25, seed=12,
               node_capacity=1 << 17)
     runs = []
-    for amin in (2, 0):
+    for adaptive in (True, False):
         x = om.BatchedMCTS(256, **kw)
         x.engine.set_chain_split(4, 16)
-        x.engine.set_adaptive_extra_rounds(amin)
+        x.engine.set_adaptive_extra_rounds(adaptive, 0)
         x.random_openings(opening, seed=13)
         out = x.selfplay_steps(net, 6, temperature_moves=12, opening_moves=opening, emit_targets=True)
         torch.cuda.synchronize()
@@ -364,7 +365,7 @@ def test_adaptive_extra_rounds(om, opening):
     (n, r, _), out = runs[0]
     (nf, rf, _), out_f = runs[1]
     assert n == nf == 6 and rf == 6 * 26
-    assert r == (2 * 26 + 4 * 12 if opening == 4 else 6 * 26), (opening, r)
+    assert r == (2 * 26 + 4 * 10 if opening == 4 else 6 * 26), (opening, r)
     for k in out:
         assert torch.equal(out[k], out_f[k]), k
     numerics.record(f"adaptive extra rounds, {opening}-ply openings", f"{r - 60} extra rounds in 6 searches "

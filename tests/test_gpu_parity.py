@@ -448,10 +448,10 @@ def test_gpu_async_search_matches_sync(om):
         ms, launches, rows = b.engine.nn_timing()
         sel, bk, launches2 = b.engine.tree_timing()
         # every round is timed, the extra chain-splitting rounds included: 2
-        # batches per thread + X in [2, 3] per search (adaptive: the first two
+        # batches per thread + X in [0, 3] per search (adaptive: the first two
         # searches run the full 3)
         searches, rounds, finals = b.engine.round_counts()
-        assert searches == moves and moves * 4 <= rounds <= moves * 5
+        assert searches == moves and 2 * 5 + (moves - 2) * 2 <= rounds <= moves * 5
         assert launches2 == rounds * 2 and finals == moves * 2  # 2 pipeline groups at G >= 64
         timed_groups = 2  # every group's NN launches carry events
         assert launches == rounds * timed_groups

@@ -9,6 +9,6 @@ export OUT=gpurun_out/$N
 COMMON="--steps 20 --warmup 5 --sustained-moves 72 --cpu-baseline-moves 0"
 bash tools/gpu.sh "tests" || exit 1
 for r in $(seq 1 "${ROUNDS:-2}"); do
-  bash tools/gpu.sh "bench fixed8_$r $COMMON --adaptive-min 0 --chain-cuts 8" \
+  bash tools/gpu.sh "bench fixed8_$r $COMMON --fixed-extra-rounds --chain-cuts 8" \
     "bench ad2c16_$r $COMMON" "bench ad2c8_$r $COMMON --chain-cuts 8" || exit 1
 done

@@ -8,8 +8,8 @@ N=${1:-aab2}
 export OUT=gpurun_out/$N
 COMMON="--steps 20 --warmup 5 --cpu-baseline-moves 0"
 for r in $(seq 1 "${ROUNDS:-2}"); do
-  bash tools/gpu.sh "bench adapt_$r $COMMON" "bench fixed16_$r $COMMON --adaptive-min 0 --chain-cuts 16" \
-    "bench fixed8_$r $COMMON --adaptive-min 0 --chain-cuts 8" || exit 1
+  bash tools/gpu.sh "bench adapt_$r $COMMON" "bench fixed16_$r $COMMON --fixed-extra-rounds --chain-cuts 16" \
+    "bench fixed8_$r $COMMON --fixed-extra-rounds --chain-cuts 8" || exit 1
 done
 bash tools/gpu.sh "bench adapt144 $COMMON --sustained-moves 144" \
-  "bench fixed16s144 $COMMON --sustained-moves 144 --adaptive-min 0 --chain-cuts 16" || exit 1
+  "bench fixed16s144 $COMMON --sustained-moves 144 --fixed-extra-rounds --chain-cuts 16" || exit 1

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (OAMD_ADAPT_A / _B / _W were policy knobs of an intermediate build; the engine no longer reads them)
 # Adaptive extra rounds, second sweep: X = the most demand (cuts used; 2X when
 # a search used all X) over the last OAMD_ADAPT_W measured searches +
 # OAMD_ADAPT_B, against the fixed counts; ROUNDS interleaved sweeps.
@@ -13,5 +14,5 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
   OAMD_ADAPT_W=8 OAMD_ADAPT_B=2 bash tools/gpu.sh "bench w8b2_$r $COMMON" || exit 1
   OAMD_ADAPT_W=16 OAMD_ADAPT_B=2 bash tools/gpu.sh "bench w16b2_$r $COMMON" || exit 1
   OAMD_ADAPT_W=8 OAMD_ADAPT_B=4 bash tools/gpu.sh "bench w8b4_$r $COMMON" || exit 1
-  bash tools/gpu.sh "bench fixed16_$r $COMMON --adaptive-min 0 --chain-cuts 16" || exit 1
+  bash tools/gpu.sh "bench fixed16_$r $COMMON --fixed-extra-rounds --chain-cuts 16" || exit 1
 done
