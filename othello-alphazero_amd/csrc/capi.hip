@@ -169,8 +169,9 @@ struct oamd_engine {
     int steps_total = 0;  // of the step-wise search begun by oamd_engine_search_begin
     bool exact_interleaving = true;  // oamd_engine_set_exact_interleaving
     // native search, exact interleaving: an all-terminal chain stops after
-    // chain_budget re-selections in a round, at most chain_cuts times per
-    // search (k_tree); chain_cuts extra rounds per search. 0 = never split
+    // chain_budget re-selections in a round, at most X <= chain_cuts times
+    // per search (k_tree), X extra rounds per search (pick_extra_rounds).
+    // budget 0 = never split
     int chain_budget = 4;
     int chain_cuts = 16;
     // adaptive extra rounds (pick_extra_rounds): a grouped search runs X in
