@@ -96,8 +96,9 @@ def max_search_rounds(args) -> int:
     picks each search's count adaptively, capi.hip pick_extra_rounds, and
     reports the rounds it ran: oamd_engine_round_counts)."""
     steps = (args.sims + args.threads * args.batch - 1) // (args.threads * args.batch)
-    extra = args.chain_cuts if (not args.round_robin_endgames and args.chain_budget > 0
-                                and not single_game_split(args)) else 0
+    # (capi.hip extra_rounds: no game can use more cuts than T x steps / budget)
+    extra = (min(args.chain_cuts, args.threads * steps // args.chain_budget)
+             if (not args.round_robin_endgames and args.chain_budget > 0 and not single_game_split(args)) else 0)
     return steps + extra
 
 

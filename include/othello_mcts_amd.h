@@ -184,7 +184,8 @@ int oamd_engine_set_nn_chains(oamd_engine *e, int32_t chains);
  * re-selections in a round such a chain stops and the game's next round
  * resumes it exactly there (every game keeps its order of operations; only
  * round boundaries move), at most `cuts` times per search, at the cost of
- * up to `cuts` extra rounds per search (see the adaptive count below).
+ * up to `cuts` extra rounds per search (see the adaptive count below; never
+ * more than T x steps / budget, the most cuts one game's search can use).
  * Default budget 4, cuts 16; budget 0 = never split. Results do not depend on
  * it. */
 int oamd_engine_set_chain_split(oamd_engine *e, int32_t budget, int32_t cuts);

@@ -1035,7 +1035,11 @@ static GroupPlan plan_groups(oamd_engine* e) {
 // Extra rounds of a native grouped search (chain splitting, k_tree): the
 // reference's interleaving only
 static int extra_rounds(const oamd_engine* e) {
-    return e->exact_interleaving && e->chain_budget > 0 ? e->chain_cuts : 0;
+    if (!e->exact_interleaving || e->chain_budget <= 0) return 0;
+    // a cut follows >= budget all-terminal batches of its round, and a search
+    // has T x steps batches per game: no game can use more cuts than that
+    const int64_t batches = (int64_t)e->cfg.num_threads * ((e->cfg.num_simulations + e->L() - 1) / e->L());
+    return (int)std::min<int64_t>(e->chain_cuts, batches / e->chain_budget);
 }
 
 // Extra rounds X of the next grouped search. Fixed: chain_cuts. Adaptive: a
