@@ -323,11 +323,12 @@ def parse_args(argv: list[str]):
     ap.add_argument("--round-robin-endgames", action="store_true",
                     help="all-terminal batches wait for their round instead of the reference's immediate "
                          "re-selection (oamd_engine_set_exact_interleaving(0)); default: exact")
-    ap.add_argument("--chain-budget", type=int, default=4,
+    ap.add_argument("--chain-budget", type=int, default=2,
                     help="re-selections after all-terminal batches per game and round before the chain is split "
                          "(0 = never split; exact interleaving only)")
-    ap.add_argument("--chain-cuts", type=int, default=16,
-                    help="most chain splits per game and search (= most extra rounds)")
+    ap.add_argument("--chain-cuts", type=int, default=64,
+                    help="most chain splits per game and search (= most extra rounds; the engine caps it at "
+                         "threads x steps / budget)")
     ap.add_argument("--adaptive-min", type=int, default=1,
                     help="fewest extra rounds of the adaptive count (the margin over the cuts used)")
     ap.add_argument("--fixed-extra-rounds", action="store_true",

@@ -186,7 +186,7 @@ int oamd_engine_set_nn_chains(oamd_engine *e, int32_t chains);
  * round boundaries move), at most `cuts` times per search, at the cost of
  * up to `cuts` extra rounds per search (see the adaptive count below; never
  * more than T x steps / budget, the most cuts one game's search can use).
- * Default budget 4, cuts 16; budget 0 = never split. Results do not depend on
+ * Default budget 2, cuts 64; budget 0 = never split. Results do not depend on
  * it. */
 int oamd_engine_set_chain_split(oamd_engine *e, int32_t budget, int32_t cuts);
 /* Adaptive extra rounds (default on, min_rounds 1): a grouped native search

@@ -172,8 +172,8 @@ struct oamd_engine {
     // chain_budget re-selections in a round, at most X <= chain_cuts times
     // per search (k_tree), X extra rounds per search (pick_extra_rounds).
     // budget 0 = never split
-    int chain_budget = 4;
-    int chain_cuts = 16;
+    int chain_budget = 2;
+    int chain_cuts = 64;
     // adaptive extra rounds (pick_extra_rounds): a grouped search runs X in
     // [min(adapt_min, chain_cuts), chain_cuts] extra rounds (and allows X
     // cuts), X following the search two back. adapt_on = false: always

@@ -45,7 +45,7 @@ def test_roofline_uses_union_busy_time_and_timed_rows():
     t = out["tree_kernels"]
     assert t["k_tree"]["avg_launch_ms"] == pytest.approx(0.45)
     assert t["k_tree_final_backup"]["avg_launch_ms"] == pytest.approx(0.13)
-    assert t["rounds_per_search"] == 33 and t["max_rounds_per_search"] == 37
+    assert t["rounds_per_search"] == 33 and t["max_rounds_per_search"] == 50
 
 
 def test_one_chain_union_equals_summed_durations():
@@ -60,15 +60,15 @@ def test_rounds_per_search():
     count, reported as searches and rounds: the record carries the average);
     the timed region's k_resnet dispatches are the launches the engine saw."""
     a = bench.parse_args([])
-    # 25 + min(16 cuts, 2 x 25 batches / budget 4)
-    assert bench.max_search_rounds(a) == 37 and bench.pipeline_groups(a) == 2
+    # 25 + min(64 cuts, 2 x 25 batches / budget 2)
+    assert bench.max_search_rounds(a) == 50 and bench.pipeline_groups(a) == 2
     a = bench.parse_args(["--round-robin-endgames"])
     assert bench.max_search_rounds(a) == 25
     a = bench.parse_args(["--chain-budget", "0"])
     assert bench.max_search_rounds(a) == 25
     # configs[3]: 1600 sims = 50 batches per thread
     a = bench.parse_args(["--sims", "1600", "--channels", "256", "--blocks", "20"])
-    assert bench.max_search_rounds(a) == 66
+    assert bench.max_search_rounds(a) == 100
     # one game, T > 1: the thread-split schedule has no extra rounds
     a = bench.parse_args(["--games", "1"])
     assert bench.single_game_split(a) and bench.max_search_rounds(a) == 25
