@@ -192,8 +192,9 @@ int oamd_engine_set_chain_split(oamd_engine *e, int32_t budget, int32_t cuts);
 /* Adaptive extra rounds (default on, min_rounds 1): a grouped native search
  * runs X extra rounds and allows X cuts per game, X in [min(min_rounds,
  * cuts), cuts], following the search two back (read back without draining
- * the queue): X = cuts when some root of that search was within 12 empty
- * squares of the end (the endgame, where all-terminal chains appear), else
+ * the queue; the first two searches run min_rounds): X = cuts when some
+ * root of that search was within 12 empty squares of the end (the endgame,
+ * where all-terminal chains appear), else
  * the most cuts u any game used + min_rounds (2X + 2 + min_rounds when a
  * game ran out of cuts). Extra rounds past every game's last cut are empty
  * launches; a game that would need more cuts runs its last chain uncut.

@@ -181,7 +181,7 @@ struct oamd_engine {
     static constexpr int kCutSlots = 4;
     bool adapt_on = true;
     int adapt_min = 1;
-    int adapt_x = -1;        // the last X picked from a measurement (-1: none yet)
+    int adapt_x = -1;        // the last X picked from a measurement (-1: none yet: the minimum)
     // endgame threshold: at most this many empty squares on some game's root
     // (two moves before the search) -> X = chain_cuts; raised past every root
     // whose search needed cuts
@@ -1080,7 +1080,10 @@ static int pick_extra_rounds(oamd_engine* e, int* X) {
             fprintf(stderr, "adapt search %lld X %d used %d empties %d\n", (long long)q, e->cut_x[s], used, empties);
         e->cut_x[s] = -1;
     }
-    if (e->adapt_x >= 0) *X = std::clamp(e->adapt_x, std::min(e->adapt_min, *X), *X);
+    // the first two searches (nothing read back yet) run the minimum: games
+    // usually start from an opening, and a game that needs more cuts only
+    // runs a longer round
+    *X = e->adapt_x >= 0 ? std::clamp(e->adapt_x, std::min(e->adapt_min, *X), *X) : std::min(e->adapt_min, *X);
     return OAMD_OK;
 }
 
@@ -1364,7 +1367,7 @@ int oamd_engine_set_adaptive_extra_rounds(oamd_engine* e, int32_t enable, int32_
     if (min_rounds < 0 || min_rounds > 64) return fail(OAMD_INVALID_ARGUMENT, "adaptive extra rounds: min in [0, 64]");
     e->adapt_on = enable != 0;
     e->adapt_min = min_rounds;
-    e->adapt_x = -1;  // the next searches start from chain_cuts again
+    e->adapt_x = -1;  // the next two searches run the minimum
     e->adapt_empties = oamd_engine::kEndgameEmpties;
     for (int& x : e->cut_x) x = -1;
     return OAMD_OK;

@@ -342,10 +342,10 @@ def test_chain_split_keeps_every_game_identical(om):
 @pytest.mark.parametrize("opening", [4, 50])
 def test_adaptive_extra_rounds(om, opening):
     """The adaptive extra-round count (capi.hip pick_extra_rounds): the first
-    two searches run the full count; from the third on, early games
-    (4-ply openings: no terminal leaf, no cut) run none, games within
-    12 empty squares of the end (openings of 0-50 plies over 256 games: some
-    game is) the full count. Through
+    two searches run the minimum (0 here: nothing read back yet); from the
+    third on, early games (4-ply openings: no terminal leaf, no cut) run none,
+    games within 12 empty squares of the end (openings of 0-50 plies over 256
+    games: some game is) the full count. Through
     the multi-move self-play call (one pipeline group per stream), the moves
     equal those of the fixed count."""
     from othello_mcts.synthetic import alphazero_state_dict
@@ -367,7 +367,7 @@ def test_adaptive_extra_rounds(om, opening):
     # 10 batches per thread: 20 per game and search, so at most 20 / 4 = 5
     # cuts, 5 extra rounds (capi.hip extra_rounds), whatever chain_cuts says
     assert n == nf == 6 and rf == 6 * 15
-    assert r == (2 * 15 + 4 * 10 if opening == 4 else 6 * 15), (opening, r)
+    assert r == (6 * 10 if opening == 4 else 2 * 10 + 4 * 15), (opening, r)
     for k in out:
         assert torch.equal(out[k], out_f[k]), k
     numerics.record(f"adaptive extra rounds, {opening}-ply openings", f"{r - 60} extra rounds in 6 searches "

@@ -449,7 +449,7 @@ def test_gpu_async_search_matches_sync(om):
         sel, bk, launches2 = b.engine.tree_timing()
         # every round is timed, the extra chain-splitting rounds included: 2
         # batches per thread + X in [1, 3] per search (adaptive: the first two
-        # searches run the full 3)
+        # searches run the minimum, 1)
         searches, rounds, finals = b.engine.round_counts()
         assert searches == moves and moves * 3 <= rounds <= moves * 5
         assert launches2 == rounds * 2 and finals == moves * 2  # 2 pipeline groups at G >= 64
