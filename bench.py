@@ -60,23 +60,15 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 PUBLISHED_SIMS_PER_S = 28000.0
 
 
-# the sources each kernel's committed PMC traffic record was measured on
-# (profiles/traffic_*.json carry this hash; a record of other code is not used)
-KERNEL_SOURCES = {
-    "resnet": ["resnet.hip", "kernels.h"],
-    "tree": ["tree.hip", "engine.h", "bitboard.h", "rng.h", "kernels.h"],
-}
-
-
 def kernel_hash(kind: str) -> str:
-    """sha256 (16 hex digits) over the HIP sources of one kernel family."""
-    import hashlib
+    """sha256 (16 hex digits) over the HIP sources of one kernel family, as
+    compiled into the LOADED liboamd.so (othello_mcts/provenance.py; the
+    committed PMC traffic records profiles/traffic_*.json carry it, a record
+    of other code is not used). EngineWorkload first checks that the library
+    was built from the sources on disk."""
+    from othello_mcts import provenance
 
-    h = hashlib.sha256()
-    for name in KERNEL_SOURCES[kind]:
-        h.update(name.encode())
-        h.update((ROOT / "othello-alphazero_amd" / "csrc" / name).read_bytes())
-    return h.hexdigest()[:16]
+    return provenance.loaded_hash(kind)
 
 
 def pipeline_groups(args) -> int:
@@ -132,7 +124,7 @@ def usable_cpus() -> dict:
 
 
 def cpu_baseline(history: int, C: int, R: int, hidden: int, moves: int = 24, warmup_moves: int = 2,
-                 threads: int | None = None, max_seconds: float = 120.0) -> dict:
+                 threads: int | None = None, max_seconds: float = 120.0, seed: int = 1) -> dict:
     """Oracle port of the reference CPU path (configs[0]): 1 game from the
     initial position, 2 threads x 16, 800 sims/move, eps 0.25, fp32 torch-CPU
     ResNet; `warmup_moves` untimed moves, then `moves` timed ones (stopping
@@ -146,7 +138,7 @@ def cpu_baseline(history: int, C: int, R: int, hidden: int, moves: int = 24, war
 
     import oracle as O
     import resnet_ref
-    from othello_mcts.synthetic import alphazero_state_dict
+    from othello_mcts.synthetic import live_state_dict
 
     cpus = usable_cpus()
     if threads is None:
@@ -155,7 +147,7 @@ def cpu_baseline(history: int, C: int, R: int, hidden: int, moves: int = 24, war
     torch.set_num_threads(threads)
     try:
         sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
-              alphazero_state_dict(1, 1 + 2 * history, C, R, hidden).items()}
+              live_state_dict(seed, 1 + 2 * history, C, R, hidden).items()}
 
         def nn(feat):
             with torch.no_grad():
@@ -189,7 +181,8 @@ def cpu_baseline(history: int, C: int, R: int, hidden: int, moves: int = 24, war
             "affinity_cpus": cpus["affinity_cpus"], "cgroup_quota_cpus": cpus["cgroup_quota_cpus"],
             "moves": done, "warmup_moves": warmup_moves,
             "sample": f"1 game from the initial position, {warmup_moves} warm-up + {done} timed moves x 800 sims "
-                      f"(T=2 x B=16, eps=0.25), {C}x{R + 1}b fp32 torch-CPU with {threads} threads, {dt:.1f} s"}
+                      f"(T=2 x B=16, eps=0.25), {C}x{R + 1}b fp32 torch-CPU with {threads} threads "
+                      f"(the bench's live net, seed {seed}), {dt:.1f} s"}
 
 
 def cpu_model() -> str:
@@ -227,9 +220,9 @@ def grouped() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
-def timed_max(world: int, run, sync, device: str) -> float:
+def timed_max(world: int, run, sync, device: str) -> tuple[float, float]:
     """Run `run()` bracketed by barrier + device sync on both sides; return the
-    MAX wall time over ranks (the whole job's time)."""
+    MAX wall time over ranks (the whole job's time) and this rank's own."""
     if grouped():
         dist.barrier()
     sync()
@@ -238,16 +231,22 @@ def timed_max(world: int, run, sync, device: str) -> float:
     sync()
     if grouped():
         dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    own = time.perf_counter() - t0
+    t = torch.tensor([own], dtype=torch.float64, device=device)
     if grouped():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return float(t.item()), own
 
 
-def rank_table(world: int, rank: int, device_id: str, sims: int) -> list[dict]:
-    """[{rank, device, sims}] of every rank (all_gather_object over the job's
-    process group): which physical device each rank ran on and its units."""
+def rank_table(world: int, rank: int, device_id: str, sims: int, own_s: float | None = None) -> list[dict]:
+    """[{rank, device, sims, ms, sims_per_s}] of every rank (all_gather_object
+    over the job's process group): which physical device each rank ran on, its
+    units and its own time over the barrier-bracketed region (the line's value
+    uses the MAX over ranks; a slow rank shows here)."""
     me = {"rank": rank, "device": device_id, "sims": sims}
+    if own_s is not None:
+        me["ms"] = round(own_s * 1e3, 3)
+        me["sims_per_s"] = round(sims / own_s, 1)
     if not grouped():
         return [me]
     out: list = [None] * world
@@ -343,6 +342,15 @@ def parse_args(argv: list[str]):
                     help="after the timed region, continue the same games this many more moves (endgames, "
                          "restarts) and report them as the line's `sustained` sub-record (0 = skip)")
     ap.add_argument("--seed", type=int, default=2025)
+    ap.add_argument("--net", default="live", choices=["live", "frontier", "torch-default"],
+                    help="synthetic weights of the headline workload (bench_state_dict)")
+    ap.add_argument("--policy-sharpness", type=float, default=1.25,
+                    help="the frontier net's prior sharpness (deep_tree; mean largest prior ~0.4)")
+    ap.add_argument("--deep-tree-moves", type=int, default=20,
+                    help="moves of the deep_tree sub-record from fresh openings (then --sustained-moves more; "
+                         "0 = skip it)")
+    ap.add_argument("--latency-moves", type=int, default=20,
+                    help="moves per setting of the single-game latency sub-record (0 = skip it)")
     ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
     ap.add_argument("--per-move-calls", action="store_true",
                     help="one search + selfplay_move call pair per step instead of one multi-move call")
@@ -407,19 +415,50 @@ def main(argv: list[str] | None = None) -> None:
     return report(args, world, rank, backend, EngineWorkload(args, rank, local))
 
 
+NET_KINDS = ("live", "frontier", "torch-default")
+
+
+def bench_state_dict(kind: str, seed: int, in_ch: int, C: int, R: int, hidden: int, sharpness: float = 1.25) -> dict:
+    """Seeded synthetic weights of the benched AlphaZeroNet architecture:
+    "live" (the headline net: He-scaled convs, BN statistics of real positions,
+    a value head spread over [-1, 1], near-uniform priors;
+    synthetic.live_state_dict), "frontier" (the deep_tree net: the same tower
+    with priors peaked on plausible moves like a trained net's) or
+    "torch-default" (round 1-4's init: the tower forgets its input, constant
+    value, uniform priors — kept for comparison only)."""
+    from othello_mcts.synthetic import alphazero_state_dict, live_state_dict
+
+    if kind == "live":
+        return live_state_dict(seed, in_ch, C, R, hidden)
+    if kind == "frontier":
+        return live_state_dict(seed, in_ch, C, R, hidden, policy="frontier", policy_sharpness=sharpness)
+    if kind == "torch-default":
+        return alphazero_state_dict(seed, in_ch, C, R, hidden)
+    raise ValueError(kind)
+
+
 class EngineWorkload:
     """configs[1] on this rank's GPU: `games` self-play games, one step = one
     search of every game + the on-device self-play move."""
 
-    def __init__(self, args, rank: int, local: int) -> None:
+    def __init__(self, args, rank: int, local: int, net_kind: str | None = None) -> None:
         import othello_mcts as om
-        from othello_mcts.synthetic import alphazero_state_dict
+        from othello_mcts import provenance
+
+        # the loaded liboamd.so must be the one built from the sources on disk
+        # (tools/gpu.sh benchvar swaps in prebuilt A/B variants and says so)
+        if os.environ.get("OAMD_AB_VARIANT"):
+            self.source_hashes = {"variant": os.environ["OAMD_AB_VARIANT"]}
+        else:
+            self.source_hashes = provenance.check_loaded_library()
 
         self.args = args
         self.local = local
+        self.net_kind = net_kind or args.net
         R = args.blocks - 1
-        sd = alphazero_state_dict(args.seed, 1 + 2 * args.history, args.channels, R, args.hidden)
-        self.net = om.NativeNet(sd, device=local, dtype=args.dtype)
+        self.sd = bench_state_dict(self.net_kind, args.seed, 1 + 2 * args.history, args.channels, R, args.hidden,
+                                   args.policy_sharpness)
+        self.net = om.NativeNet(self.sd, device=local, dtype=args.dtype)
         engine_seed, opening_seed = shard_seeds(args.seed, rank)
         self.b = om.BatchedMCTS(args.games, history_size=args.history, num_simulations=args.sims,
                                 num_threads=args.threads, batch_size=args.batch, seed=engine_seed)
@@ -458,13 +497,14 @@ class EngineWorkload:
     def start_measuring(self, every: int | None = None) -> None:
         e = self.b.engine
         e.enable_timing(max(1, self.args.timing_every if every is None else every))
-        self.t0 = (e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy(), e.round_counts())
+        self.t0 = (e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy(), e.round_counts(),
+                   e.descent_depths())
 
     def stop_measuring(self) -> dict:
         e = self.b.engine
-        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), (bu0, bl0), (sc0, ro0, fl0) = self.t0
-        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), (bu1, bl1), (sc1, ro1, fl1) = (
-            e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy(), e.round_counts())
+        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), (bu0, bl0), (sc0, ro0, fl0), (lv0, ds0, _) = self.t0
+        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), (bu1, bl1), (sc1, ro1, fl1), (lv1, ds1, dmax) = (
+            e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy(), e.round_counts(), e.descent_depths())
         overflow_games, depth_capped = e.status()
         if overflow_games or depth_capped:
             raise SystemExit(f"bench invalid: {overflow_games} game(s) overflowed their node pool, "
@@ -473,41 +513,89 @@ class EngineWorkload:
                 "nn_rows": rw1 - rw0, "select_ms": se1 - se0,
                 "backup_ms": bk1 - bk0, "tree_launches": tl1 - tl0, "final_launches": fl1 - fl0,
                 "searches": sc1 - sc0, "rounds": ro1 - ro0, "sims": si1 - si0, "evals": ev1 - ev0,
-                "overflow_games": overflow_games}
+                "overflow_games": overflow_games,
+                "depth_mean": (ds1 - ds0) / max(1, lv1 - lv0), "depth_max_since_start": dmax}
+
+    def prior_stats(self, n: int = 256) -> dict:
+        """The net's outputs on n real positions (the native kernel itself):
+        value spread, mean largest prior, prior mass on legal moves."""
+        import numpy as np
+
+        import othello_mcts as om
+        from othello_mcts.synthetic import calibration_features
+
+        x = calibration_features(n, self.args.history, self.args.seed + 17)
+        out = self.net(torch.from_numpy(x).to(f"cuda:{self.local}"))
+        p = out["policy"].float().cpu().numpy()
+        v = out["value"].float().cpu().numpy()
+        legal = np.zeros((n, 65), bool)
+        bits = [1 << (63 - s) for s in range(64)]
+        for i in range(n):  # planes 1, 2: black / white; plane 0: white to move
+            b = sum(bits[s] for s in range(64) if x[i, 1].flat[s] > 0)
+            w = sum(bits[s] for s in range(64) if x[i, 2].flat[s] > 0)
+            me, opp = (w, b) if x[i, 0, 0, 0] > 0 else (b, w)
+            lm = om.get_legal_moves(me, opp)
+            legal[i, :64] = [(lm >> (63 - s)) & 1 == 1 for s in range(64)]
+            legal[i, 64] = lm == 0
+        mass = (p * legal).sum(1)
+        share = (p * legal).max(1) / np.maximum(mass, 1e-30)
+        return {"positions": n, "value_std": round(float(v.std()), 4), "value_mean": round(float(v.mean()), 4),
+                "mean_max_prior": round(float(p.max(1).mean()), 4),
+                "mean_legal_mass": round(float(mass.mean()), 4),
+                "mean_max_legal_share": round(float(share.mean()), 4),
+                "policy_entropy_nats": round(float(-(p * np.log(np.maximum(p, 1e-30))).sum(1).mean()), 3)}
 
 
-def report(args, world: int, rank: int, backend: str, wl) -> None:
-    L = args.threads * args.batch
-    sims_per_search = L * ((args.sims + L - 1) // L)
-    def steps(n: int) -> None:
+def run_window(args, wl, world: int, backend: str, n: int, every: int | None = None) -> tuple[float, float, dict | None]:
+    """n steps of `wl` in a barrier-bracketed region, the engine's counters
+    over it: (max-over-ranks seconds, this rank's seconds, measurements)."""
+    measuring = hasattr(wl, "start_measuring")
+    if measuring:
+        wl.start_measuring(every)
+
+    def run():
         if hasattr(wl, "steps"):
             wl.steps(n)
         else:
             for _ in range(n):
                 wl.step()
 
-    steps(args.warmup)
+    dt_max, own = timed_max(world, run, wl.sync, "cuda" if backend == "nccl" else "cpu")
+    return dt_max, own, (wl.stop_measuring() if measuring else None)
+
+
+def park_barrier(group) -> None:
+    """Barrier over a gloo group: waiting ranks block in a socket read (no host
+    core spins) while rank 0 times the CPU baseline."""
+    if group is not None:
+        dist.barrier(group=group)
+
+
+def report(args, world: int, rank: int, backend: str, wl) -> None:
+    L = args.threads * args.batch
+    sims_per_search = L * ((args.sims + L - 1) // L)
+    dev = "cuda" if backend == "nccl" else "cpu"
+    # a host-side group for parking ranks without spinning (RCCL's barrier
+    # waits on the device); the dry run's default group is gloo already
+    park = None
+    if grouped():
+        park = dist.new_group(backend="gloo") if backend == "nccl" else dist.group.WORLD
+    if hasattr(wl, "steps"):
+        wl.steps(args.warmup)
+    else:
+        for _ in range(args.warmup):
+            wl.step()
     wl.sync()
-    measuring = hasattr(wl, "start_measuring")
-    if measuring:
-        wl.start_measuring()
-
-    def run():
-        steps(args.steps)
-
-    dt_max = timed_max(world, run, wl.sync, "cuda" if backend == "nccl" else "cpu")
-    m = wl.stop_measuring() if measuring else None
+    dt_max, own, m = run_window(args, wl, world, backend, args.steps)
     sustained = None
-    if measuring and args.sustained_moves > 0:
+    if m is not None and args.sustained_moves > 0:
         # the engine's real workload: the same games played on through their
         # endgames (all-terminal batches, chain splitting) and restarts (the
         # roofline covers every launch; HIP events sample every 5th search)
-        wl.start_measuring()
-        dt_s = timed_max(world, lambda: steps(args.sustained_moves), wl.sync,
-                         "cuda" if backend == "nccl" else "cpu")
-        sustained = sustained_fields(args, wl.stop_measuring(), world, sims_per_search, dt_s)
+        dt_s, _, ms_ = run_window(args, wl, world, backend, args.sustained_moves)
+        sustained = sustained_fields(args, ms_, world, sims_per_search, dt_s)
     value = aggregate_rate(world, args.games, sims_per_search, args.steps, dt_max)
-    ranks = rank_table(world, rank, wl.device_id, args.games * sims_per_search * args.steps)
+    ranks = rank_table(world, rank, wl.device_id, args.games * sims_per_search * args.steps, own)
     check_ranks(args, world, backend, ranks)
     n_devices = len({r["device"] for r in ranks})
     workload = (f"{args.games} concurrent self-play games per GPU, {args.sims} sims/move, "
@@ -516,6 +604,11 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
                 + (f", eval batch {args.eval_batch}" if args.eval_batch else "")
                 + (" (BASELINE configs[1])" if (args.games, args.channels, args.blocks, args.sims, args.dtype,
                                                 args.eval_batch) == (256, 128, 10, 800, "bf16", 0) else ""))
+    net_note = {"live": "seeded live-init (He-scaled convs, BN statistics of real positions, value spread over "
+                        "[-1, 1]; synthetic.live_state_dict)",
+                "frontier": "seeded live-init with priors peaked on frontier squares (synthetic.live_state_dict "
+                            "policy='frontier')",
+                "torch-default": "seeded torch-default init (degenerate: constant value, uniform priors)"}[args.net]
     result = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -530,7 +623,7 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
         "baseline_ref": {"value": PUBLISHED_SIMS_PER_S, "unit": "simulations/s",
                          "hardware": "1x RTX 4090 + 24-core CPU (reference README.md:25, BASELINE.md)"},
         "dtype": args.dtype,
-        "data": (f"synthetic: seeded random-init {args.channels}x{args.blocks}b AlphaZeroNet weights, "
+        "data": (f"synthetic: {net_note} {args.channels}x{args.blocks}b AlphaZeroNet weights, "
                  "random openings (0-8 plies)") if m is not None else
                 "DRY RUN: rank plumbing only, no GPU work (each step a fixed sleep); not a measurement",
         "config": {
@@ -538,6 +631,7 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
             "games_per_gpu": args.games,
             "sims_per_move": args.sims,
             "leaves_per_step": L,
+            "net_init": args.net,
             "parallelism": (f"games sharded over {world} rank(s) on {n_devices} GPU(s), no collective"
                             + (" (REHEARSAL: ranks share GPUs; not a scaling point)"
                                if n_devices < world else "")),
@@ -557,16 +651,112 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
         result["dry_run"] = True
     if m is not None:
         result.update(measured_fields(args, m, workload))
+        result["net_outputs"] = wl.prior_stats()
         if sustained is not None:
             result["sustained"] = sustained
-        if rank == 0 and world == 1 and args.cpu_baseline_moves > 0:
+        if args.deep_tree_moves > 0:
+            result["deep_tree"] = deep_tree_record(args, wl, world, rank, backend, sims_per_search)
+        if args.latency_moves > 0 and rank == 0:
+            result["latency"] = latency_record(args, wl)
+    # the CPU baseline on rank 0 at every world size, after every timed region;
+    # the other ranks wait at a gloo barrier (blocked, not spinning)
+    if args.cpu_baseline_moves > 0 and (m is not None or args.dry_run):
+        if rank == 0:
+            dry = args.dry_run
             result["cpu_baseline"] = cpu_baseline(args.history, args.channels, args.blocks - 1, args.hidden,
-                                                  moves=args.cpu_baseline_moves,
-                                                  threads=args.cpu_baseline_threads or None)
+                                                  moves=1 if dry else args.cpu_baseline_moves,
+                                                  warmup_moves=0 if dry else 2,
+                                                  threads=args.cpu_baseline_threads or None, seed=args.seed)
+            if dry:
+                result["cpu_baseline"]["note"] = "dry run: 1 move, no warm-up (plumbing only)"
+            result["cpu_baseline"]["world_size"] = world
+        park_barrier(park)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if grouped():
         dist.destroy_process_group()
+
+
+def deep_tree_record(args, wl, world: int, rank: int, backend: str, sims_per_search: int) -> dict:
+    """the same configs[1] engine with a net whose priors are
+    peaked like a trained one's (synthetic.live_state_dict policy='frontier'):
+    tree shape (descent depth), k_tree time per round against the ResNet's busy
+    time per launch, and whether the tree rounds still hide behind the other
+    pipeline group's ResNet launches (step time vs the union busy time)."""
+    import copy
+    import gc
+
+    del wl.b
+    gc.collect()
+    torch.cuda.synchronize()
+    dw = EngineWorkload(args, rank, wl.local, net_kind="frontier")
+    dw.steps(args.warmup)
+    dw.sync()
+    out = {"net": f"frontier, policy_sharpness {args.policy_sharpness}", "net_outputs": dw.prior_stats()}
+    for name, n in (("from_openings", args.deep_tree_moves), ("sustained", args.sustained_moves)):
+        if n <= 0:
+            continue
+        dt, _, m = run_window(args, dw, world, backend, n, every=1)
+        a = copy.copy(args)
+        a.steps = n  # the window's own moves (rows launched)
+        mf = measured_fields(a, m, "")
+        step_ms = dt * 1e3 / n
+        busy_per_step = m["nn_busy_ms"] / n
+        tree_round_ms = m["select_ms"] / max(1, m["tree_launches"])
+        out[name] = {
+            "moves": n,
+            "value": round(aggregate_rate(world, args.games, sims_per_search, n, dt), 1),
+            "unit": "simulations/s",
+            "ms_per_step": round(step_ms, 3),
+            "depth_mean": round(m["depth_mean"], 3),
+            "depth_max": m["depth_max_since_start"],
+            "k_tree_ms_per_round": round(tree_round_ms, 4),
+            "resnet_busy_ms_per_launch": mf["roofline"]["busy_ms_per_launch"],
+            "resnet_busy_union_ms_per_step": round(busy_per_step, 3),
+            "step_over_busy": round(step_ms / max(busy_per_step, 1e-9), 4),
+            "k_tree_hidden": bool(step_ms <= 1.05 * busy_per_step),
+            "rounds_per_search": mf["tree_kernels"]["rounds_per_search"],
+            "terminal_share": mf["work"]["terminal_share"],
+            "frac": mf["roofline"]["frac"],
+        }
+    out["note"] = ("timed on every search (HIP events on every round: the event packets lengthen the launch "
+                   "gaps ~10 us, so this rate is a little below an untimed run's); depth = levels below the root of "
+                   "every selected leaf; k_tree_hidden: step time within 5 % of the union of the ResNet launches' "
+                   "busy intervals")
+    del dw
+    return out
+
+
+def latency_record(args, wl) -> dict:
+    """Single-game latency through the drop-in MCTS (reference README.md:25:
+    < 30 ms per 800-simulation action; player.py:208-259 evaluation at 3200
+    sims, eps 0, README.md:195): median / p90 ms per search + visit_counts
+    over `latency_moves` moves of one game (argmax play), the headline net."""
+    import othello_mcts as om
+
+    out = {"published": "< 30 ms per 800-simulation action, 1x RTX 4090 + 24-core CPU (README.md:25)"}
+    for name, sims, eps in (("selfplay_800", 800, 0.25), ("evaluation_3200", 3200, 0.0)):
+        mc = om.MCTS(history_size=args.history, torch_device=f"cuda:{wl.local}", num_simulations=sims, num_threads=2,
+                     batch_size=16, dirichlet_epsilon=eps, seed=3)
+        mc.search(wl.net)  # warm-up
+        mc.reset_position()
+        ms = []
+        for _ in range(args.latency_moves):
+            if mc.position().is_terminal():
+                mc.reset_position()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            mc.search(wl.net)
+            vc = mc.visit_counts()  # the result on the host, as the caller sees it
+            ms.append((time.perf_counter() - t0) * 1e3)
+            acts = mc.position().legal_actions()
+            mc.apply_action(acts[max(range(len(vc)), key=vc.__getitem__)])
+        ms.sort()
+        out[name] = {"sims": sims, "threads": 2, "batch_size": 16, "dirichlet_epsilon": eps, "moves": len(ms),
+                     "median_ms": round(ms[len(ms) // 2], 3), "p90_ms": round(ms[min(len(ms) - 1, int(len(ms) * 0.9))], 3),
+                     "min_ms": round(ms[0], 3)}
+        del mc
+    return out
 
 
 def sustained_fields(args, m: dict, world: int, sims_per_search: int, dt_max: float) -> dict:
@@ -666,7 +856,9 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     return {
         "overflow_games": m["overflow_games"],
         "work": {"simulations": m["sims"], "n_eval": m["evals"], "rows_launched": rows_launched,
-                 "terminal_share": round(1.0 - eval_share, 5)},
+                 "terminal_share": round(1.0 - eval_share, 5),
+                 # tree shape: levels below the root of every selected leaf
+                 "depth_mean": round(m["depth_mean"], 3), "depth_max_since_start": m["depth_max_since_start"]},
         "roofline": {
             "bound": "mfma",
             "kernel": "k_resnet_w8 (fused 19-conv tower + heads, 8-wave geometry)",
@@ -681,6 +873,7 @@ def measured_fields(args, m: dict, workload: str) -> dict:
             "launches": m["busy_launches"],
             "timed_region_launches": m["busy_launches"],
             "kernel_hash": kernel_hash("resnet"),
+            "library_source_hash": kernel_hash("all"),
             "avg_launch_ms": round(avg_ms, 4),
             "busy_ms_per_launch": round(busy_ms, 4),
             "nn_chains": args.nn_chains,

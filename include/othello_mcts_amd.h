@@ -40,6 +40,10 @@ typedef enum oamd_status {
 
 const char *oamd_last_error(void);
 int oamd_abi_version(void);
+/* Hash of the sources the library was built from (16 hex digits; family
+ * "resnet", "tree" or "all", else NULL): build.py compiles them in, and
+ * othello_mcts.provenance compares them with the sources on disk. */
+const char *oamd_source_hash(const char *family);
 /* number of visible HIP devices (0 when no GPU) */
 int oamd_device_count(int32_t *out);
 
@@ -163,43 +167,16 @@ int oamd_engine_search(oamd_engine *e, oamd_net *net, int64_t *simulations, int6
  * step-wise. The reference counts neither; it builds no NN row for a terminal
  * leaf (search_thread.cpp:88-90). */
 int oamd_engine_work_counters(oamd_engine *e, int64_t *simulations, int64_t *evaluations);
-/* Split the games into `groups` pipeline groups (own HIP streams) so that tree
- * kernels of one group overlap the NN launch of another (0 = auto: 2 groups
- * from 64 games, else 1; at most 8). Results do not depend on it. */
-int oamd_engine_set_pipeline(oamd_engine *e, int32_t groups);
+/* Tree shape since the engine was created (host outputs; waits for the
+ * engine's stream): leaves selected (= simulations), the sum of their descent
+ * depths (levels below the root, search_thread.cpp:64-67) and the deepest
+ * descent. mean depth = depth_sum / leaves. */
+int oamd_engine_descent_depths(oamd_engine *e, int64_t *leaves, int64_t *depth_sum, int32_t *depth_max);
 /* Rows per ResNet launch in oamd_engine_search (0 = a whole pipeline group per
  * launch): a group's rows are evaluated by consecutive launches of at most
  * `rows` rows on its stream (the NN evaluation batch; configs[4] uses 2048).
  * Results do not depend on it. */
 int oamd_engine_set_nn_batch(oamd_engine *e, int32_t rows);
-/* The pipeline groups' ResNet launches form `chains` chains (group k in chain
- * k % chains, 1..4, default 2): launches of one chain run one after another,
- * chains run concurrently (the default lets the two groups' launches overlap
- * at their ends). Results do not depend on it. */
-int oamd_engine_set_nn_chains(oamd_engine *e, int32_t chains);
-/* Native search with the exact interleaving: a virtual thread whose batches
- * come back all terminal selects again at once (search_thread.cpp:102-127),
- * which near a game's end can run a thread's whole remaining search inside one
- * round and hold its pipeline group's ResNet launch. After `budget`
- * re-selections in a round such a chain stops and the game's next round
- * resumes it exactly there (every game keeps its order of operations; only
- * round boundaries move), at most `cuts` times per search, at the cost of
- * up to `cuts` extra rounds per search (see the adaptive count below; never
- * more than T x steps / budget, the most cuts one game's search can use).
- * Default budget 2, cuts 64; budget 0 = never split. Results do not depend on
- * it. */
-int oamd_engine_set_chain_split(oamd_engine *e, int32_t budget, int32_t cuts);
-/* Adaptive extra rounds (default on, min_rounds 1): a grouped native search
- * runs X extra rounds and allows X cuts per game, X in [min(min_rounds,
- * cuts), cuts], following the search two back (read back without draining
- * the queue; the first two searches run min_rounds): X = cuts when some
- * root of that search was within 12 empty squares of the end (the endgame,
- * where all-terminal chains appear), else
- * the most cuts u any game used + min_rounds (2X + 2 + min_rounds when a
- * game ran out of cuts). Extra rounds past every game's last cut are empty
- * launches; a game that would need more cuts runs its last chain uncut.
- * enable = 0: X = cuts always. Scheduling only: results are identical. */
-int oamd_engine_set_adaptive_extra_rounds(oamd_engine *e, int32_t enable, int32_t min_rounds);
 /* Counts since the engine was created: grouped native searches enqueued (all
  * pipeline groups of one search count once), their NN rounds (steps + extra
  * rounds each), and the final backup-only k_tree launches of the timed
@@ -215,21 +192,6 @@ int oamd_engine_round_counts(const oamd_engine *e, int64_t *searches, int64_t *r
  * search rounds stay hidden behind the other pipeline group's ResNet launch
  * in sustained self-play. */
 int oamd_engine_set_exact_interleaving(oamd_engine *e, int32_t enable);
-/* Workgroups of the chain-splitting extra rounds' ResNet launches (default
- * 128; 0 = the regular grid, the list's capacity): those launches hold the
- * rows of lagging games only (none outside endgames), so a small grid loops
- * over them instead of dispatching ~1000 mostly empty workgroups between the
- * other NN chain's. Scheduling only: results are identical. */
-int oamd_engine_set_extra_round_grid(oamd_engine *e, int32_t workgroups);
-/* Diagnostics: copy the ResNet kernel's per-workgroup time stamps (8 u64 per
- * workgroup, 16 u64 per workgroup: see tools/nn_stamps.py) of the last launch. Only in builds
- * with OAMD_EXTRA_FLAGS=-DOAMD_STAMPS; otherwise OAMD_INVALID_ARGUMENT. */
-int oamd_debug_read_stamps(uint64_t *out, int64_t n);
-/* Diagnostics: k_tree's phase cycle sums over every wave since the last reset
- * (tools/tree_stamps.py); reset != 0 zeroes them after the copy. Only in
- * builds with OAMD_EXTRA_FLAGS=-DOAMD_TREE_STAMPS; otherwise
- * OAMD_INVALID_ARGUMENT. */
-int oamd_debug_tree_stamps(uint64_t *out, int64_t n, int32_t reset);
 
 /* Step-wise search for an external evaluator (the Python NeuralNet callback
  * path, othello_mcts.cpp:36-45). Rows: row = game * L + leaf, L =

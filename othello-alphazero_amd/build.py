@@ -82,17 +82,33 @@ def newer(out: Path, deps: list[Path]) -> bool:
     return out.exists() and all(out.stat().st_mtime >= d.stat().st_mtime for d in deps)
 
 
+def source_hash_defines() -> list[str]:
+    """-D flags carrying the source hashes (othello_mcts/provenance.py) into
+    capi.hip, so the library reports what it was built from."""
+    sys.path.insert(0, str(PKG))
+    try:
+        import provenance
+    finally:
+        sys.path.pop(0)
+    return [f'-DOAMD_SOURCE_HASH_{k.upper()}="{provenance.source_hash(k)}"' for k in provenance.FAMILIES]
+
+
 def build(jobs: int = 4, force: bool = False) -> None:
     BUILD.mkdir(exist_ok=True)
-    headers = list(CSRC.glob("*.h")) + [INCLUDE / "othello_mcts_amd.h"]
+    headers = list(CSRC.glob("*.h")) + [INCLUDE / "othello_mcts_amd.h", INCLUDE / "othello_mcts_amd_experimental.h"]
+    hashes = source_hash_defines()
     objs = []
     todo = []
+    all_srcs = [CSRC / u for u in UNITS] + headers
     for unit, extra in UNITS.items():
         src = CSRC / unit
         obj = BUILD / (unit + ".o")
         objs.append(obj)
-        if force or not newer(obj, [src, *headers, Path(__file__)]):
-            todo.append([HIPCC, *COMMON, *extra, "-c", str(src), "-o", str(obj)])
+        # capi.hip carries the hashes of every source: rebuilt when any changes
+        deps = all_srcs if unit == "capi.hip" else [src, *headers]
+        if force or not newer(obj, [*deps, Path(__file__)]):
+            todo.append([HIPCC, *COMMON, *extra, *(hashes if unit == "capi.hip" else []), "-c", str(src),
+                         "-o", str(obj)])
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(run, todo))
     lib = PKG / "liboamd.so"
@@ -105,7 +121,7 @@ def build(jobs: int = 4, force: bool = False) -> None:
     ext = sysconfig.get_config_var("EXT_SUFFIX")
     mod = PKG / f"_othello_mcts_impl{ext}"
     src = CSRC / "pybind_module.cpp"
-    if force or not newer(mod, [src, INCLUDE / "othello_mcts_amd.h", lib, Path(__file__)]):
+    if force or not newer(mod, [src, *headers, lib, Path(__file__)]):
         run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
              "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], "-I", str(INCLUDE),
              str(src), "-o", str(mod), "-L", str(PKG), "-loamd", "-Wl,-rpath,$ORIGIN"])

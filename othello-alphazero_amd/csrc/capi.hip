@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/othello_mcts_amd.h"
+#include "../../include/othello_mcts_amd_experimental.h"
 #include "bitboard.h"
 
 #include "engine.h"
@@ -22,7 +23,11 @@
 using namespace oamd;
 
 constexpr int kMaxPipeline = 8;
-constexpr int kEvPerBlock = 4;  // timing events per (round, group): tree begin/end, NN begin/end
+constexpr int kEvPerBlock = 4;
+// device counters (k_tree): [0..1] sims / NN rows of the current search,
+// [2..3] cumulative, [4..5] of timed searches, [6] summed descent depths,
+// [7] deepest descent
+constexpr int kCounters = 8;  // timing events per (round, group): tree begin/end, NN begin/end
 // Order of the pipeline groups' NN launches within an NN chain (one chain:
 // one after another, each owning every CU while the other groups' tree
 // kernels run beside it). OAMD_NN_ORDER 1: a token event passed between the
@@ -512,6 +517,20 @@ extern "C" {
 const char* oamd_last_error(void) { return g_err.c_str(); }
 int oamd_abi_version(void) { return OAMD_ABI_VERSION; }
 
+// build.py passes the source hashes (othello_mcts/provenance.py)
+#ifndef OAMD_SOURCE_HASH_ALL
+#define OAMD_SOURCE_HASH_ALL "unknown"
+#define OAMD_SOURCE_HASH_RESNET "unknown"
+#define OAMD_SOURCE_HASH_TREE "unknown"
+#endif
+const char* oamd_source_hash(const char* family) {
+    if (!family) return nullptr;
+    if (!std::strcmp(family, "all")) return OAMD_SOURCE_HASH_ALL;
+    if (!std::strcmp(family, "resnet")) return OAMD_SOURCE_HASH_RESNET;
+    if (!std::strcmp(family, "tree")) return OAMD_SOURCE_HASH_TREE;
+    return nullptr;
+}
+
 int oamd_device_count(int32_t* out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
@@ -819,7 +838,7 @@ int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity,
     e->seed = seed;
     const size_t nodes = (size_t)num_games * node_capacity;
     if ((rc = dalloc(&e->link, nodes)) || (rc = dalloc(&e->stat, nodes)) || (rc = dalloc(&e->pos, nodes)) ||
-        (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) || (rc = dalloc(&e->counters, 6)) ||
+        (rc = dalloc(&e->games, num_games)) || (rc = dalloc(&e->explore_tab, kExploreTab)) || (rc = dalloc(&e->counters, kCounters)) ||
         (rc = dalloc(&e->rowcount, 2 * kMaxPipeline)) ||
         (rc = dalloc(&e->status_dev, 2)) || (rc = dalloc(&e->info_dev, num_games)) || (rc = dalloc(&e->visits_dev, (size_t)num_games * 65)) ||
         (rc = dalloc(&e->q_dev, (size_t)num_games * 65)) ||
@@ -828,7 +847,7 @@ int oamd_engine_create(int32_t device, int32_t num_games, int64_t node_capacity,
         delete e;
         return rc;
     }
-    if (hipMemset(e->counters, 0, 6 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMemset(e->counters, 0, kCounters * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(e->rowcount, 0, 2 * kMaxPipeline * sizeof(int32_t)) != hipSuccess) {
         delete e;
         return fail(OAMD_RUNTIME, "engine init: counter memset failed");
@@ -1325,6 +1344,17 @@ int oamd_engine_work_counters(oamd_engine* e, int64_t* sims, int64_t* evals) {
     HIPCHK(hipStreamSynchronize(e->stream));
     if (sims) *sims = (int64_t)c[0];
     if (evals) *evals = (int64_t)c[1];
+    return OAMD_OK;
+}
+
+int oamd_engine_descent_depths(oamd_engine* e, int64_t* leaves, int64_t* depth_sum, int32_t* depth_max) {
+    DeviceGuard dg(e->device);
+    unsigned long long c[kCounters] = {};
+    HIPCHK(hipMemcpyAsync(c, e->counters, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (leaves) *leaves = (int64_t)c[2];
+    if (depth_sum) *depth_sum = (int64_t)c[6];
+    if (depth_max) *depth_max = (int32_t)c[7];
     return OAMD_OK;
 }
 

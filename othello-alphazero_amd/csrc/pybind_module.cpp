@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "othello_mcts_amd.h"
+#include "othello_mcts_amd_experimental.h"
 
 namespace py = pybind11;
 using namespace py::literals;
@@ -450,6 +451,11 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
     m.def("get_flips", &oamd_host_flips, "move_mask"_a, "player_discs"_a, "opponent_discs"_a);
     m.def("device_count", &device_count);
     m.def("abi_version", &oamd_abi_version);
+    m.def("source_hash", [](const std::string& family) {
+        const char* h = oamd_source_hash(family.c_str());
+        if (!h) throw py::value_error("unknown source family: " + family);
+        return std::string(h);
+    });
 
     py::class_<Position>(m, "Position")
         .def_static("initial_position", &Position::initial_position)
@@ -698,6 +704,12 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
             int64_t sims = 0, evals = 0;
             check(oamd_engine_work_counters(e.h, &sims, &evals));
             return py::make_tuple(sims, evals);
+        })
+        .def("descent_depths", [](Engine& e) {
+            int64_t leaves = 0, dsum = 0;
+            int32_t dmax = 0;
+            check(oamd_engine_descent_depths(e.h, &leaves, &dsum, &dmax));
+            return py::make_tuple(leaves, dsum, dmax);
         })
         .def("tree_timing", [](Engine& e) {
             float sel, bk;

@@ -242,7 +242,8 @@ __device__ __forceinline__ void append_rows(const EngineView& E, int* cnt, int l
 __device__ __forceinline__ void select_range(const EngineView& E, int g, GameState* gs, size_t base,
                                              int i0, int i1, uint64_t& event, int hist_node,
                                              int hist_n, unsigned long long& sims,
-                                             unsigned long long& evals, int* cnt, int list_base) {
+                                             unsigned long long& evals, int* cnt, int list_base,
+                                             unsigned long long& depth_sum, int& depth_max) {
     const int lane = lane_id();
     const int root = gs->root;
     const uint64_t key = gs->key;
@@ -355,6 +356,8 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
         write_packed_features(E, base, r, d, p0, p1, hist_node, hist_n, lk.player, t, valid);
         sims += 1;
         evals += valid ? 1 : 0;
+        depth_sum += (unsigned long long)d;
+        depth_max = d > depth_max ? d : depth_max;
         if (cnt) {
             valid_rows |= (uint64_t)(valid ? 1 : 0) << (i - c0);
             if (i - c0 == 63 || i == i1 - 1) {
@@ -569,7 +572,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     uint64_t event = gs->event;
     const int hist_n = gs->hist_n;
     const int hist_node = lane < 16 ? gs->hist[lane] : -1;
-    unsigned long long sims = 0, evals = 0;
+    unsigned long long sims = 0, evals = 0, depth_sum = 0;
+    int depth_max = 0;
     int count = gs->count;
     bool overflow = false;
     const int nt = t1 - t0;
@@ -611,7 +615,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
             const unsigned long long ev0 = evals;
             TS_T(tsel0);
             select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals, cnt_add,
-                         g0 * E.L);
+                         g0 * E.L, depth_sum, depth_max);
             TS_T(tsel1);
             TS_ADD(kTsSelect, tsel1 - tsel0);
             TS_ADD(kTsBatches, 1);
@@ -669,6 +673,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
             if (timed) {  // [4..5] the searches that record timing events
                 atomicAdd(E.counters + 4, sims);
                 atomicAdd(E.counters + 5, evals);
+            }
+            // [6] descent depths summed over every selected leaf, [7] the
+            // deepest descent (levels below the root; oamd_engine_descent_depths)
+            if (sims) {
+                atomicAdd(E.counters + 6, depth_sum);
+                atomicMax(E.counters + 7, (unsigned long long)depth_max);
             }
         }
     }

@@ -248,6 +248,55 @@ def make_resnet_large() -> None:
     (GOLD / "resnet_large_meta.json").write_text(json.dumps(meta, indent=1))
 
 
+def make_resnet_live() -> None:
+    """The benched live nets (bench.py bench_state_dict: "live" for the headline
+    and configs[3], "frontier" for the deep_tree record)
+    against the reference's own AlphaZeroNet at throughput-geometry sizes. The
+    weights are regenerated by the tests (synthetic.live_state_dict, float64
+    calibration rounded to float32) and checked against the stored checksum;
+    the planes likewise (ref_fixtures.real_features)."""
+    import hashlib
+
+    import torch
+
+    sys.path.insert(0, str(REF_PY))
+    from othello_alphazero.neural_net import AlphaZeroNet  # reference, read-only
+
+    from othello_mcts.synthetic import live_state_dict, net_config_from_state_dict
+    from ref_fixtures import planes_checksum
+
+    torch.set_num_threads(8)
+    cases = {
+        # name: (policy, sharpness, weight seed, H, C, blocks, hidden, rows, planes seed)
+        "live_c128b9_h8_r1027": ("random", 1.0, 2025, 8, 128, 9, 128, 1027, 81),
+        "frontier_c128b9_h8_r1027": ("frontier", 1.25, 2025, 8, 128, 9, 128, 1027, 82),
+        "live_c256b19_h8_r1025": ("random", 1.0, 2025, 8, 256, 19, 256, 1025, 83),
+    }
+    meta, arrays = {}, {}
+    for name, (policy, sharp, seed, H, C, R, hid, n, xseed) in cases.items():
+        sd = live_state_dict(seed, 1 + 2 * H, C, R, hid, policy=policy, policy_sharpness=sharp)
+        h = hashlib.sha256()
+        for k, v in sd.items():
+            h.update(k.encode())
+            h.update(np.ascontiguousarray(v).tobytes())
+        net = AlphaZeroNet(**net_config_from_state_dict(sd))
+        net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+        net.eval()
+        x = _real_features(n, H, xseed)
+        with torch.no_grad():
+            out = net(torch.from_numpy(x))
+        arrays[f"{name}_policy"] = out["policy"].numpy()
+        arrays[f"{name}_value"] = out["value"].numpy()
+        meta[name] = {"policy": policy, "policy_sharpness": sharp, "seed": seed, "history_size": H,
+                      "conv_channels": C, "num_residual_blocks": R, "value_head_hidden_channels": hid,
+                      "boards": n, "planes_seed": xseed, "planes_sha256_16": planes_checksum(x),
+                      "weights_sha256_16": h.hexdigest()[:16],
+                      "value_std": float(out["value"].std()), "mean_max_prior": float(out["policy"].max(1).values.mean())}
+        print("resnet live", name, meta[name]["value_std"], meta[name]["mean_max_prior"])
+    np.savez_compressed(GOLD / "resnet_live.npz", **arrays)
+    (GOLD / "resnet_live_meta.json").write_text(json.dumps(meta, indent=1))
+
+
 def make_mcts_known_answers() -> None:
     data = {
         "provenance": "SURVEY.md section 4 (measured with the compiled reference extension)",
@@ -267,10 +316,14 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["resnet_large"]:
         make_resnet_large()
         raise SystemExit(0)
+    if sys.argv[1:] == ["resnet_live"]:
+        make_resnet_live()
+        raise SystemExit(0)
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "ref", "all"], check=True)
     make_bitboards()
     make_features()
     make_strings_errors()
     make_resnet()
     make_resnet_large()
+    make_resnet_live()
     make_mcts_known_answers()

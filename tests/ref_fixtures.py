@@ -51,6 +51,37 @@ def planes_checksum(x: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(x.astype(np.int8)).tobytes()).hexdigest()[:16]
 
 
+def weights_checksum(sd) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for k, v in sd.items():
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(v).tobytes())
+    return h.hexdigest()[:16]
+
+
+def live_case(name: str):
+    """(meta, state_dict, planes, golden) of a live-net golden
+    (resnet_live.*, make_golden.py make_resnet_live): the weights regenerate
+    from their seed (synthetic.live_state_dict) and the planes from theirs,
+    both checked against the stored checksums."""
+    from othello_mcts.synthetic import live_state_dict
+
+    meta = json.loads((GOLD / "resnet_live_meta.json").read_text())[name]
+    sd = live_state_dict(meta["seed"], 1 + 2 * meta["history_size"], meta["conv_channels"],
+                         meta["num_residual_blocks"], meta["value_head_hidden_channels"], policy=meta["policy"],
+                         policy_sharpness=meta["policy_sharpness"])
+    assert weights_checksum(sd) == meta["weights_sha256_16"], "live_state_dict no longer reproduces the golden's weights"
+    x = real_features(meta["boards"], meta["history_size"], meta["planes_seed"])
+    assert planes_checksum(x) == meta["planes_sha256_16"]
+    g = np.load(GOLD / "resnet_live.npz")
+    return meta, sd, x, {"policy": g[f"{name}_policy"], "value": g[f"{name}_value"]}
+
+
+LIVE_CASES = ["live_c128b9_h8_r1027", "frontier_c128b9_h8_r1027", "live_c256b19_h8_r1025"]
+
+
 def load_cases() -> list[dict]:
     return json.loads((GOLD / "ref_mcts.json").read_text())["cases"]
 

@@ -23,7 +23,8 @@ def _m(launches=66, busy_per=0.75, span_per=1.05, rows=4096, evals_share=0.9, st
             "busy_launches": launches * steps, "nn_rows": rows * launches,
             "select_ms": 0.45 * 33 * 2, "backup_ms": 0.13 * 2, "tree_launches": 33 * 2, "final_launches": 2,
             "searches": steps, "rounds": 33 * steps,
-            "sims": 256 * 800 * steps, "evals": int(256 * 800 * steps * evals_share), "overflow_games": 0}
+            "sims": 256 * 800 * steps, "evals": int(256 * 800 * steps * evals_share), "overflow_games": 0,
+            "depth_mean": 4.2, "depth_max_since_start": 17}
 
 
 def test_roofline_uses_union_busy_time_and_timed_rows():
@@ -41,6 +42,7 @@ def test_roofline_uses_union_busy_time_and_timed_rows():
     share = out["work"]["n_eval"] / out["work"]["rows_launched"]
     assert r["achieved_rows_launched"] == pytest.approx(r["achieved"] / share, rel=1e-3)
     assert out["work"]["terminal_share"] == pytest.approx(0.1, abs=1e-3)
+    assert out["work"]["depth_mean"] == 4.2 and out["work"]["depth_max_since_start"] == 17
     # tree: 33 select rounds per search and group (8 extra), one final backup each
     t = out["tree_kernels"]
     assert t["k_tree"]["avg_launch_ms"] == pytest.approx(0.45)

@@ -21,13 +21,41 @@ def u(x):
 
 
 def test_abi_exports_every_declared_symbol():
-    header = (ROOT / "include" / "othello_mcts_amd.h").read_text()
-    names = set(re.findall(r"\b(oamd_[a-z0-9_]+)\s*\(", header))
+    names = set()
+    for h in sorted((ROOT / "include").glob("*.h")):
+        names |= set(re.findall(r"\b(oamd_[a-z0-9_]+)\s*\(", h.read_text()))
     assert len(names) > 30
     lib = ctypes.CDLL(str(PKG / "othello_mcts" / "liboamd.so"))
     missing = [n for n in sorted(names) if not hasattr(lib, n)]
     assert not missing, missing
     assert lib.oamd_abi_version() == 1
+
+
+def test_product_header_has_no_tuning_or_debug_entry_points():
+    """the product ABI is the reference's surface plus the
+    batched / self-play / measurement API; scheduling knobs and diagnostics
+    live in othello_mcts_amd_experimental.h."""
+    product = (ROOT / "include" / "othello_mcts_amd.h").read_text()
+    names = set(re.findall(r"\b(oamd_[a-z0-9_]+)\s*\(", product))
+    assert not [n for n in names if n.startswith("oamd_debug_")]
+    for n in ("oamd_engine_set_pipeline", "oamd_engine_set_nn_chains", "oamd_engine_set_chain_split",
+              "oamd_engine_set_adaptive_extra_rounds", "oamd_engine_set_extra_round_grid"):
+        assert n not in names, n
+
+
+def test_loaded_library_was_built_from_the_sources_on_disk():
+    """build.py compiles the source hashes into
+    liboamd.so; the loaded library must report the hashes of the sources on
+    disk (a stale prebuilt library fails here, in smoke() and in bench.py)."""
+    from othello_mcts import provenance
+
+    got = provenance.check_loaded_library()
+    assert set(got) == {"resnet", "tree", "all"}
+    assert all(len(v) == 16 for v in got.values())
+    lib = ctypes.CDLL(str(PKG / "othello_mcts" / "liboamd.so"))
+    lib.oamd_source_hash.restype = ctypes.c_char_p
+    assert lib.oamd_source_hash(b"all").decode() == got["all"]
+    assert lib.oamd_source_hash(b"nope") is None
 
 
 def test_abi_device_count_without_gpu_is_safe():

@@ -49,13 +49,23 @@ def _check_two_rank_line(out: dict, steps: int, step_ms: float, games: int) -> N
     assert [r["rank"] for r in ranks] == [0, 1]
     assert len({r["device"] for r in ranks}) == 2
     assert all(r["sims"] == games * 800 * steps for r in ranks)
+    # per-rank time and rate: rank 1 sleeps twice as long
+    assert all(r["ms"] > 0 and abs(r["sims_per_s"] - r["sims"] / (r["ms"] / 1e3)) <= 1e-3 * r["sims_per_s"] + 0.1
+               for r in ranks)
+    assert ranks[1]["ms"] >= steps * 2 * step_ms and ranks[0]["ms"] >= steps * step_ms
     # the max over ranks: rank 1 sleeps 2 x step_ms per step
     dt = out["ms_per_step"] * steps / 1e3
     assert dt >= steps * 2 * step_ms / 1e3
     # whole-job rate = both ranks' units / the max time
     assert abs(out["value"] - 2 * games * 800 * steps / dt) <= 1e-3 * out["value"] + 0.1
     assert "REHEARSAL" not in out["config"]["parallelism"] and out["config"]["backend"] == "gloo"
-    assert "roofline" not in out and "cpu_baseline" not in out
+    assert "roofline" not in out
+    # the CPU baseline rides on every world size's line (rank 0, after the
+    # timed regions, the other ranks parked at a gloo barrier); a dry run
+    # times one move of it
+    cb = out["cpu_baseline"]
+    assert cb["world_size"] == 2 and cb["moves"] == 1 and cb["value"] > 0 and cb["kind"] == "port"
+    assert "dry run" in cb["note"]
 
 
 def test_bare_bench_gpus2_starts_its_own_ranks():
@@ -113,8 +123,8 @@ def test_single_rank_helpers():
     assert bench.shard_seeds(2025, 0) != bench.shard_seeds(2025, 1)
     assert bench.aggregate_rate(8, 256, 800, 10, 2.0) == 8 * 256 * 800 * 10 / 2.0
     calls = []
-    dt = bench.timed_max(1, lambda: calls.append(1), lambda: calls.append(0), "cpu")
-    assert calls == [0, 1, 0] and dt >= 0.0
+    dt, own = bench.timed_max(1, lambda: calls.append(1), lambda: calls.append(0), "cpu")
+    assert calls == [0, 1, 0] and dt >= 0.0 and own == dt
     cpus = bench.usable_cpus()
     assert 1 <= cpus["usable"] <= cpus["nproc"]
     cmd = bench.launch_command(4, ["--gpus", "4"], 1234)

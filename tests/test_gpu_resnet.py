@@ -82,6 +82,36 @@ def test_throughput_geometry_vs_reference_golden(om, golden_dir, name, dtype):
     assert dp <= tp and dv <= tv
 
 
+# live nets (value spread ~0.5, priors up to peaked): errors scale with the
+# outputs' spread, so these tolerances are their own
+LIVE_TOL = {"bf16": (2e-2, 5e-2), "fp16": (4e-3, 1e-2)}
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("name", ["live_c128b9_h8_r1027", "frontier_c128b9_h8_r1027", "live_c256b19_h8_r1025"])
+def test_live_nets_vs_reference_golden(om, name, dtype):
+    """The nets bench.py runs (live value heads, the deep_tree
+    net's peaked priors) against the reference's own AlphaZeroNet on >= 1025
+    real positions in the throughput geometries (make_golden.py
+    make_resnet_live; weights and planes regenerated, checksum-checked)."""
+    import ref_fixtures as RF
+
+    meta, sd, x, g = RF.live_case(name)
+    net = om.NativeNet(sd, device=0, dtype=dtype)
+    out = net(torch.from_numpy(x).to(DEV))
+    torch.cuda.synchronize()
+    p, v = out["policy"].cpu().numpy(), out["value"].cpu().numpy()
+    dp = np.abs(p - g["policy"]).max()
+    dv = np.abs(v - g["value"]).max()
+    # relative to the output's own scale: the largest prior / the value spread
+    numerics.record(f"resnet live golden {name} {dtype}",
+                    f"max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e} (value std {g['value'].std():.3f}, "
+                    f"mean max prior {g['policy'].max(1).mean():.3f}, rms dvalue {np.sqrt(((v - g['value'])**2).mean()):.2e})")
+    assert v.std() > 0.3  # live on the GPU too
+    tp, tv = LIVE_TOL[dtype]
+    assert dp <= tp and dv <= tv
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("rows", [1, 3, 4, 5, 257, 1027, 2048])
 def test_native_net_vs_torch_fp32_restatement(om, rows, dtype):

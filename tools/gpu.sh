@@ -84,7 +84,8 @@ run_recipe() {
       for r in $(seq ${ROUNDS:-2}); do
         for v in ${AB_ORDER:-$(ls abv)}; do
           cp abv/$v/liboamd.so $PKG/liboamd.so
-          step 600 "$OUT/benchvar_${n}_${v}_$r.json" python bench.py --cpu-baseline-moves 0 "$@" || { restore_lib; return 1; }
+          step 600 "$OUT/benchvar_${n}_${v}_$r.json" env OAMD_AB_VARIANT=$v python bench.py --cpu-baseline-moves 0 \
+            --deep-tree-moves 0 --latency-moves 0 "$@" || { restore_lib; return 1; }
         done
       done
       restore_lib ;;
