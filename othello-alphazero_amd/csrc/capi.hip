@@ -199,12 +199,31 @@ struct oamd_engine {
     int cut_x[kCutSlots] = {-1, -1, -1, -1};  // X of the search in the slot (-1: slot empty)
     int cut_groups[kCutSlots] = {};
     hipEvent_t cuts_ev[kCutSlots][kMaxPipeline] = {};
+    // allocated into locals and published only when every allocation
+    // succeeded (a failure leaves nothing half-initialised behind)
     int ensure_cut_slots() {
         if (cuts_dev) return OAMD_OK;
-        if (int rc = dalloc(&cuts_dev, (size_t)2 * kCutSlots * kMaxPipeline)) return rc;
-        HIPCHK(hipHostMalloc((void**)&cuts_host, sizeof(int32_t) * 2 * kCutSlots * kMaxPipeline));
-        for (auto& row : cuts_ev)
-            for (auto& x : row) HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+        int32_t* dev = nullptr;
+        int32_t* host = nullptr;
+        hipEvent_t evs[kCutSlots][kMaxPipeline] = {};
+        int rc = dalloc(&dev, (size_t)2 * kCutSlots * kMaxPipeline);
+        if (!rc && hipHostMalloc((void**)&host, sizeof(int32_t) * 2 * kCutSlots * kMaxPipeline) != hipSuccess)
+            rc = fail(OAMD_RUNTIME, "cut slots: hipHostMalloc failed");
+        for (auto& row : evs)
+            for (auto& x : row)
+                if (!rc && hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
+                    rc = fail(OAMD_RUNTIME, "cut slots: hipEventCreate failed");
+        if (rc) {
+            for (auto& row : evs)
+                for (auto x : row)
+                    if (x) (void)hipEventDestroy(x);
+            if (host) (void)hipHostFree(host);
+            dfree(dev);
+            return rc;
+        }
+        cuts_host = host;
+        std::memcpy(cuts_ev, evs, sizeof(evs));
+        cuts_dev = dev;
         return OAMD_OK;
     }
     // workgroups of an extra round's ResNet launch (0 = the regular grid)
@@ -249,10 +268,22 @@ struct oamd_engine {
     // restarts; the busy time is the union over the whole window (launches of
     // the pipeline groups' searches overlap in time, and the groups drift
     // apart over whole games, so per-search unions would count shared time
-    // twice). A search's slots are contiguous: [group][round][launch].
-    static constexpr int64_t kSpanChunk = 1 << 15;  // slots (2 x u64) per chunk
-    std::vector<unsigned long long*> span_chunks;
-    int64_t span_used = 0;      // slot index where the next search's block starts
+    // twice). A search's slots are contiguous: [group][round][launch], in one
+    // chunk of at least kSpanChunk slots (larger when one search needs more).
+    // Chunks that no search reserves in any more are copied to the host once
+    // (span_ticks); a window of more than kSpanWindow slots stops recording
+    // and makes oamd_engine_nn_busy fail (its launches would be missing).
+    static constexpr int64_t kSpanChunk = 1 << 15;    // slots (2 x u64) per chunk
+    static constexpr int64_t kSpanWindow = 1 << 23;   // most slots of one window (128 MiB)
+    struct SpanChunk {
+        unsigned long long* p = nullptr;
+        int64_t cap = 0, used = 0;
+    };
+    std::vector<SpanChunk> span_chunks;
+    int64_t span_slots = 0;     // slots reserved in this window
+    int64_t span_dropped = 0;   // launches of this window that found no slot
+    size_t span_copied = 0;     // leading chunks already folded into span_ticks
+    std::vector<std::pair<long long, long long>> span_ticks;  // their intervals (ticks)
     int ev_cur = 0;
     float nn_ms = 0.0f;
     float select_ms = 0.0f;
@@ -299,29 +330,57 @@ struct oamd_engine {
     // n contiguous span slots for one search (nullptr when timing is off)
     int reserve_spans(int64_t n, unsigned long long** out) {
         *out = nullptr;
-        if (!timing || n <= 0 || n > kSpanChunk) return OAMD_OK;
-        int64_t c = span_used / kSpanChunk, off = span_used % kSpanChunk;
-        if (off + n > kSpanChunk) {
-            ++c;
-            off = 0;
+        if (!timing || n <= 0) return OAMD_OK;
+        if (span_slots + n > kSpanWindow) {  // not recorded: nn_busy reports it
+            span_dropped += n;
+            return OAMD_OK;
         }
-        while ((int64_t)span_chunks.size() <= c) {
-            unsigned long long* x = nullptr;
-            if (int rc = dalloc(&x, (size_t)2 * kSpanChunk)) return rc;
-            HIPCHK(hipMemset(x, 0, sizeof(unsigned long long) * 2 * kSpanChunk));
-            span_chunks.push_back(x);
+        if (span_chunks.empty() || span_chunks.back().used + n > span_chunks.back().cap) {
+            SpanChunk c;
+            c.cap = std::max(kSpanChunk, n);
+            if (int rc = dalloc(&c.p, (size_t)2 * c.cap)) return rc;
+            if (hipMemset(c.p, 0, sizeof(unsigned long long) * 2 * c.cap) != hipSuccess) {
+                dfree(c.p);
+                return fail(OAMD_RUNTIME, "span window: hipMemset failed");
+            }
+            span_chunks.push_back(c);
         }
-        *out = span_chunks[c] + 2 * off;
-        span_used = c * kSpanChunk + off + n;
+        SpanChunk& c = span_chunks.back();
+        *out = c.p + 2 * c.used;
+        c.used += n;
+        span_slots += n;
         return OAMD_OK;
     }
     // restart the window: every launch that may still write a slot is done
     int reset_spans() {
-        if (!span_used) return OAMD_OK;
+        if (span_chunks.empty() && !span_dropped) return OAMD_OK;
         HIPCHK(hipDeviceSynchronize());
-        for (int64_t c = 0; c * kSpanChunk < span_used; ++c)
-            HIPCHK(hipMemset(span_chunks[c], 0, sizeof(unsigned long long) * 2 * kSpanChunk));
-        span_used = 0;
+        for (auto& c : span_chunks) dfree(c.p);
+        span_chunks.clear();
+        span_slots = span_dropped = 0;
+        span_copied = 0;
+        span_ticks.clear();
+        return OAMD_OK;
+    }
+    // the window's recorded intervals (ticks); waits for the device
+    int span_intervals(std::vector<std::pair<long long, long long>>* iv) {
+        HIPCHK(hipDeviceSynchronize());  // every launch of the window has written its slot
+        auto read = [&](const SpanChunk& c, std::vector<std::pair<long long, long long>>* to) -> int {
+            std::vector<unsigned long long> sp((size_t)2 * c.used);
+            if (c.used)
+                HIPCHK(hipMemcpy(sp.data(), c.p, sizeof(unsigned long long) * 2 * c.used, hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < c.used; ++i)  // start stored complemented (an atomicMin on zeroed slots)
+                if (sp[2 * i + 1]) to->emplace_back((long long)~sp[2 * i], (long long)sp[2 * i + 1]);
+            return OAMD_OK;
+        };
+        // chunks before the last one are complete: fold them in once
+        for (; span_copied + 1 < span_chunks.size(); ++span_copied) {
+            if (int rc = read(span_chunks[span_copied], &span_ticks)) return rc;
+            dfree(span_chunks[span_copied].p);
+        }
+        *iv = span_ticks;
+        if (!span_chunks.empty())
+            if (int rc = read(span_chunks.back(), iv)) return rc;
         return OAMD_OK;
     }
 
@@ -453,7 +512,7 @@ struct oamd_engine {
         dfree(spd_dev);
         for (auto& pool : ev)
             for (auto e : pool) (void)hipEventDestroy(e);
-        for (auto& x : span_chunks) dfree(x);
+        for (auto& c : span_chunks) dfree(c.p);
         if (cuts_dev) {
             (void)hipDeviceSynchronize();  // no copy into cuts_host in flight
             dfree(cuts_dev);
@@ -988,22 +1047,14 @@ int oamd_engine_nn_timing(const oamd_engine* ce, float* nn_ms, int64_t* launches
 int oamd_engine_nn_busy(const oamd_engine* ce, float* busy_ms, int64_t* launches) {
     oamd_engine* e = const_cast<oamd_engine*>(ce);
     DeviceGuard dg(e->device);
-    std::vector<std::pair<float, float>> iv;
-    if (e->span_used) {
-        HIPCHK(hipDeviceSynchronize());  // every launch of the window has written its slot
-        std::vector<unsigned long long> sp((size_t)2 * e->span_used);
-        for (int64_t c = 0; c * oamd_engine::kSpanChunk < e->span_used; ++c) {
-            const int64_t n = std::min(oamd_engine::kSpanChunk, e->span_used - c * oamd_engine::kSpanChunk);
-            HIPCHK(hipMemcpy(sp.data() + 2 * c * oamd_engine::kSpanChunk, e->span_chunks[c],
-                             sizeof(unsigned long long) * 2 * n, hipMemcpyDeviceToHost));
-        }
-        unsigned long long t0 = ~0ULL;
-        for (int64_t i = 0; i < e->span_used; ++i)
-            if (sp[2 * i + 1]) t0 = std::min(t0, ~sp[2 * i]);
-        for (int64_t i = 0; i < e->span_used; ++i)  // 100 MHz ticks -> ms, from the window's first start
-            if (sp[2 * i + 1]) iv.emplace_back((float)((~sp[2 * i] - t0) * 1e-5), (float)((sp[2 * i + 1] - t0) * 1e-5));
-    }
-    if (busy_ms) *busy_ms = (float)interval_union(iv);
+    if (e->span_dropped)
+        return fail(OAMD_RUNTIME, "nn_busy: the timing window outgrew its " + std::to_string(oamd_engine::kSpanWindow) +
+                                      " slots; " + std::to_string(e->span_dropped) +
+                                      " launches were not recorded (restart it with oamd_engine_enable_timing)");
+    std::vector<std::pair<long long, long long>> iv;
+    if (int rc = e->span_intervals(&iv)) return rc;
+    // 100 MHz ticks -> ms, once for the whole union
+    if (busy_ms) *busy_ms = (float)(interval_union(iv) * 1e-5);
     // the launches that ran (a search reserves slots for the most launches of
     // any group per round; groups of unequal size may leave some unused)
     if (launches) *launches = (int64_t)iv.size();
@@ -1091,7 +1142,11 @@ static int pick_extra_rounds(oamd_engine* e, int* X) {
         // cuts used + the minimum, or 2X + 2 when a game ran out of cuts
         // (k_tree reports X + 1: X = 0 still counts the chains that would
         // have been split)
+        // the raised threshold decays by one per search without cuts back to
+        // kEndgameEmpties (a mid-game chain must not pin the full
+        // count for the engine's lifetime)
         if (used > 0) e->adapt_empties = std::max(e->adapt_empties, empties + 3);
+        else if (e->adapt_empties > oamd_engine::kEndgameEmpties) --e->adapt_empties;
         if (empties <= e->adapt_empties) e->adapt_x = e->chain_cuts;
         else e->adapt_x = (used > e->cut_x[s] ? 2 * e->cut_x[s] + 2 : used) + e->adapt_min;
         static const bool plog = getenv("OAMD_ADAPT_LOG") != nullptr;

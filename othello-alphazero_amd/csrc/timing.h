@@ -6,15 +6,18 @@
 #include <utility>
 #include <vector>
 
-// Total length covered by a set of [begin, end] intervals (ms, any sign:
-// they are measured from one group's first event, and another pipeline
-// group's stream may run ahead of it). The ResNet launches of different NN
-// chains overlap; their union is the time some launch ran.
-inline double interval_union(std::vector<std::pair<float, float>>& iv) {
+// Total length covered by a set of [begin, end] intervals (any sign: they
+// may be measured from one group's first event, and another pipeline group's
+// stream may run ahead of it). The ResNet launches of different NN chains
+// overlap; their union is the time some launch ran. The engine passes int64
+// clock ticks (exact over any window; ADVICE r4: float ms lost 0.01-0.06 ms of
+// resolution over minutes-long windows) and converts the sum once.
+template <typename T>
+inline double interval_union(std::vector<std::pair<T, T>>& iv) {
     std::sort(iv.begin(), iv.end());
     double sum = 0.0;
     bool open = false;
-    float lo = 0.0f, hi = 0.0f;
+    T lo = T(0), hi = T(0);
     for (const auto& x : iv) {
         if (!open || x.first > hi) {
             if (open) sum += (double)hi - lo;

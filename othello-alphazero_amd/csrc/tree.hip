@@ -55,7 +55,15 @@ __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)
 // no wait for it on gfx950 (it emits none; a wave's vector memory operations
 // reach the cache in order), so the stores' write-back overlaps the next
 // descent's first loads instead of a vmcnt(0) drain per leaf.
+// -DOAMD_TREE_DRAIN restores the vmcnt(0) drain (the A/B build that
+// shows both orderings give identical results; tests/test_cpu_host.py checks
+// in the ISA that k_tree reads no statistics through the scalar cache, which
+// would not see these vector stores).
+#ifdef OAMD_TREE_DRAIN
+__device__ __forceinline__ void wave_order() { wait_stores(); }
+#else
 __device__ __forceinline__ void wave_order() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+#endif
 
 // Wave reductions with DPP (row_shr / row_bcast inclusive scan, the total ends
 // in lane 63): a few cycles per step, where __shfl_xor compiles to a chain of

@@ -356,3 +356,38 @@ def test_type_stub_covers_the_reference_surface_and_the_module():
               "legal_actions", "apply_move", "apply_pass", "apply_action", "is_terminal", "__str__"):
         params("Position", m)
         assert hasattr(impl.Position, m)
+
+
+def test_k_tree_reads_no_written_state_through_the_scalar_cache(tmp_path):
+    """k_tree orders each leaf's statistic stores before the next
+    descent's loads with a wavefront fence, not a vmcnt(0) drain (tree.hip
+    wave_order). That holds for VECTOR loads (a wave's vector memory
+    operations reach the cache in order); a load the compiler turned into a
+    scalar s_load goes through the scalar cache, which does not see the wave's
+    vector stores. Check the gfx950 ISA of the built k_tree: every s_load reads
+    the kernel arguments (s[0:1]) or GameState.key / .event (offsets 0x10 /
+    0x18), which k_tree reads once before its own stores. A compiler that
+    scalarises a statistic or link load fails this test (build with
+    OAMD_EXTRA_FLAGS=-DOAMD_TREE_DRAIN, the drained ordering, until reviewed)."""
+    import subprocess
+
+    llvm = "/opt/rocm/lib/llvm/bin"
+    obj = PKG / "build" / "tree.hip.o"
+    fat, co = tmp_path / "tree.fatbin", tmp_path / "tree.co"
+    subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", str(obj), str(tmp_path / "x.o")],
+                   check=True)
+    subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", "--no-show-raw-insn", str(co)], check=True,
+                         capture_output=True, text=True).stdout
+    body, inside = [], False
+    for ln in dis.splitlines():
+        if ln.endswith(">:"):
+            inside = "6k_tree" in ln
+        elif inside:
+            body.append(ln.strip())
+    assert len(body) > 1000, "k_tree not found in the disassembly"
+    scalar = [ln for ln in body if ln.startswith(("s_load", "s_buffer_load"))]
+    other = [ln for ln in scalar if not re.search(r",\s*s\[0:1\],", ln)]
+    offsets = {ln.rsplit(",", 1)[1].split("//")[0].strip() for ln in other}
+    assert offsets <= {"0x10", "0x18"}, other

@@ -22,7 +22,8 @@ import resnet_ref
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-TOL = {"bf16": (2e-2, 5e-2), "fp16": (4e-3, 1e-2)}  # the live nets' (tests/test_gpu_resnet.py LIVE_TOL)
+# the live nets' (tests/test_gpu_resnet.py LIVE_TOL: C=256's 39 convs double the value's)
+TOL = {"bf16": (5e-3, 2e-1), "fp16": (1e-3, 2e-2)}
 
 
 def _bench_sd(C, R, hid):

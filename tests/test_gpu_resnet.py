@@ -82,9 +82,16 @@ def test_throughput_geometry_vs_reference_golden(om, golden_dir, name, dtype):
     assert dp <= tp and dv <= tv
 
 
-# live nets (value spread ~0.5, priors up to peaked): errors scale with the
-# outputs' spread, so these tolerances are their own
-LIVE_TOL = {"bf16": (2e-2, 5e-2), "fp16": (4e-3, 1e-2)}
+# live nets (value spread ~0.5, priors up to peaked): the bf16 (fp16)
+# rounding of the tower's activations between its 19 convs dominates (an fp32
+# emulation of the kernel's roundings reproduces the GPU's errors: value rms
+# 0.0135, max 0.062 at bf16), so these tolerances are their own:
+# max |dpolicy|, max |dvalue|, rms dvalue, per dtype and tower depth (19 / 39
+# convs; measured C=128 bf16 8e-4-2.5e-3 / 0.057-0.067 / 0.0135-0.014, fp16
+# 2.2e-4-3.3e-4 / 0.0074-0.0085 / 0.0017-0.0019; C=256 bf16 2.4e-3 / 0.114 /
+# 0.0247)
+LIVE_TOL = {("bf16", 128): (5e-3, 1e-1, 2.5e-2), ("fp16", 128): (1e-3, 2e-2, 5e-3),
+            ("bf16", 256): (5e-3, 2e-1, 4e-2), ("fp16", 256): (1e-3, 4e-2, 8e-3)}
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
@@ -108,8 +115,8 @@ def test_live_nets_vs_reference_golden(om, name, dtype):
                     f"max|dpolicy|={dp:.2e} max|dvalue|={dv:.2e} (value std {g['value'].std():.3f}, "
                     f"mean max prior {g['policy'].max(1).mean():.3f}, rms dvalue {np.sqrt(((v - g['value'])**2).mean()):.2e})")
     assert v.std() > 0.3  # live on the GPU too
-    tp, tv = LIVE_TOL[dtype]
-    assert dp <= tp and dv <= tv
+    tp, tv, trms = LIVE_TOL[(dtype, meta["conv_channels"])]
+    assert dp <= tp and dv <= tv and np.sqrt(((v - g["value"]) ** 2).mean()) <= trms
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
