@@ -342,8 +342,10 @@ def parse_args(argv: list[str]):
                     help="after the timed region, continue the same games this many more moves (endgames, "
                          "restarts) and report them as the line's `sustained` sub-record (0 = skip)")
     ap.add_argument("--seed", type=int, default=2025)
-    ap.add_argument("--net", default="live", choices=["live", "frontier", "torch-default"],
-                    help="synthetic weights of the headline workload (bench_state_dict)")
+    ap.add_argument("--net", default="live", choices=list(NET_KINDS),
+                    help="weights of the headline workload (bench_state_dict)")
+    ap.add_argument("--deep-tree-net", default="selfplay", choices=list(NET_KINDS),
+                    help="weights of the deep_tree sub-record (default: the self-play trained net)")
     ap.add_argument("--policy-sharpness", type=float, default=1.25,
                     help="the frontier net's prior sharpness (deep_tree; mean largest prior ~0.4)")
     ap.add_argument("--deep-tree-moves", type=int, default=20,
@@ -415,23 +417,28 @@ def main(argv: list[str] | None = None) -> None:
     return report(args, world, rank, backend, EngineWorkload(args, rank, local))
 
 
-NET_KINDS = ("live", "frontier", "torch-default")
+NET_KINDS = ("live", "frontier", "selfplay", "torch-default")
 
 
 def bench_state_dict(kind: str, seed: int, in_ch: int, C: int, R: int, hidden: int, sharpness: float = 1.25) -> dict:
     """Seeded synthetic weights of the benched AlphaZeroNet architecture:
     "live" (the headline net: He-scaled convs, BN statistics of real positions,
     a value head spread over [-1, 1], near-uniform priors;
-    synthetic.live_state_dict), "frontier" (the deep_tree net: the same tower
-    with priors peaked on plausible moves like a trained net's) or
-    "torch-default" (round 1-4's init: the tower forgets its input, constant
-    value, uniform priors — kept for comparison only)."""
-    from othello_mcts.synthetic import alphazero_state_dict, live_state_dict
+    synthetic.live_state_dict), "frontier" (the same tower with priors peaked
+    on plausible moves), "selfplay" (the deep_tree net: 128x10b H=8 trained by
+    self-play, bench_nets/; synthetic.selfplay_state_dict) or "torch-default"
+    (round 1-4's init: the tower forgets its input, constant value, uniform
+    priors — kept for comparison only)."""
+    from othello_mcts.synthetic import alphazero_state_dict, live_state_dict, selfplay_state_dict
 
     if kind == "live":
         return live_state_dict(seed, in_ch, C, R, hidden)
     if kind == "frontier":
         return live_state_dict(seed, in_ch, C, R, hidden, policy="frontier", policy_sharpness=sharpness)
+    if kind == "selfplay":
+        if (in_ch, C, R, hidden) != (17, 128, 9, 128):
+            raise SystemExit("bench.py: the self-play trained net is 128x10b with history 8")
+        return selfplay_state_dict()
     if kind == "torch-default":
         return alphazero_state_dict(seed, in_ch, C, R, hidden)
     raise ValueError(kind)
@@ -608,6 +615,7 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
                         "[-1, 1]; synthetic.live_state_dict)",
                 "frontier": "seeded live-init with priors peaked on frontier squares (synthetic.live_state_dict "
                             "policy='frontier')",
+                "selfplay": "self-play trained (bench_nets/selfplay_128x10b_h8)",
                 "torch-default": "seeded torch-default init (degenerate: constant value, uniform priors)"}[args.net]
     result = {
         "metric": METRIC,
@@ -678,8 +686,8 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
 
 
 def deep_tree_record(args, wl, world: int, rank: int, backend: str, sims_per_search: int) -> dict:
-    """the same configs[1] engine with a net whose priors are
-    peaked like a trained one's (synthetic.live_state_dict policy='frontier'):
+    """the same configs[1] engine with a net whose priors and
+    values are a trained one's (default: the self-play trained net, bench_nets/):
     tree shape (descent depth), k_tree time per round against the ResNet's busy
     time per launch, and whether the tree rounds still hide behind the other
     pipeline group's ResNet launches (step time vs the union busy time)."""
@@ -689,10 +697,13 @@ def deep_tree_record(args, wl, world: int, rank: int, backend: str, sims_per_sea
     del wl.b
     gc.collect()
     torch.cuda.synchronize()
-    dw = EngineWorkload(args, rank, wl.local, net_kind="frontier")
+    dw = EngineWorkload(args, rank, wl.local, net_kind=args.deep_tree_net)
     dw.steps(args.warmup)
     dw.sync()
-    out = {"net": f"frontier, policy_sharpness {args.policy_sharpness}", "net_outputs": dw.prior_stats()}
+    desc = {"selfplay": "128x10b trained by self-play (bench_nets/selfplay_128x10b_h8, tools/selfplay_train.py: "
+                        "15k games from a live init)",
+            "frontier": f"live init, priors peaked on frontier squares (sharpness {args.policy_sharpness})"}
+    out = {"net": desc.get(args.deep_tree_net, args.deep_tree_net), "net_outputs": dw.prior_stats()}
     for name, n in (("from_openings", args.deep_tree_moves), ("sustained", args.sustained_moves)):
         if n <= 0:
             continue

@@ -307,3 +307,19 @@ def live_state_dict(
         else:
             sd[k] = np.ascontiguousarray(sd[k], dtype=np.float32)
     return sd
+
+
+# ------------------------------------------------- self-play trained net
+BENCH_NETS = __import__("pathlib").Path(__file__).resolve().parents[2] / "bench_nets"
+
+
+def selfplay_state_dict(name: str = "selfplay_128x10b_h8") -> dict[str, np.ndarray]:
+    """A 128x10b net trained by this package's own self-play loop
+    (tools/selfplay_train.py: 15k games of 800-sim self-play from a live init,
+    the reference's loss and SGD settings; bench_nets/NAME.json is its log),
+    stored as float16 with the reference's state_dict keys. Loaded without
+    unpickling (numpy.load, allow_pickle=False). Its priors sit on legal moves
+    (mass 0.99) and its value tracks game outcomes, like a trained net's."""
+    z = np.load(BENCH_NETS / f"{name}.npz", allow_pickle=False)
+    return {k: (np.array(0, dtype=np.int64) if k.endswith("num_batches_tracked")
+                else np.ascontiguousarray(z[k], dtype=np.float32)) for k in z.files}

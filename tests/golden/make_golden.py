@@ -262,19 +262,22 @@ def make_resnet_live() -> None:
     sys.path.insert(0, str(REF_PY))
     from othello_alphazero.neural_net import AlphaZeroNet  # reference, read-only
 
-    from othello_mcts.synthetic import live_state_dict, net_config_from_state_dict
+    from othello_mcts.synthetic import live_state_dict, net_config_from_state_dict, selfplay_state_dict
     from ref_fixtures import planes_checksum
 
     torch.set_num_threads(8)
     cases = {
-        # name: (policy, sharpness, weight seed, H, C, blocks, hidden, rows, planes seed)
+        # name: (policy, sharpness, weight seed, H, C, blocks, hidden, rows, planes seed); policy
+        # "selfplay": the self-play trained net of bench_nets/ (the deep_tree record's)
+        "selfplay_c128b9_h8_r1027": ("selfplay", 0.0, 0, 8, 128, 9, 128, 1027, 84),
         "live_c128b9_h8_r1027": ("random", 1.0, 2025, 8, 128, 9, 128, 1027, 81),
         "frontier_c128b9_h8_r1027": ("frontier", 1.25, 2025, 8, 128, 9, 128, 1027, 82),
         "live_c256b19_h8_r1025": ("random", 1.0, 2025, 8, 256, 19, 256, 1025, 83),
     }
     meta, arrays = {}, {}
     for name, (policy, sharp, seed, H, C, R, hid, n, xseed) in cases.items():
-        sd = live_state_dict(seed, 1 + 2 * H, C, R, hid, policy=policy, policy_sharpness=sharp)
+        sd = (selfplay_state_dict() if policy == "selfplay" else
+              live_state_dict(seed, 1 + 2 * H, C, R, hid, policy=policy, policy_sharpness=sharp))
         h = hashlib.sha256()
         for k, v in sd.items():
             h.update(k.encode())

@@ -66,12 +66,15 @@ def live_case(name: str):
     (resnet_live.*, make_golden.py make_resnet_live): the weights regenerate
     from their seed (synthetic.live_state_dict) and the planes from theirs,
     both checked against the stored checksums."""
-    from othello_mcts.synthetic import live_state_dict
+    from othello_mcts.synthetic import live_state_dict, selfplay_state_dict
 
     meta = json.loads((GOLD / "resnet_live_meta.json").read_text())[name]
-    sd = live_state_dict(meta["seed"], 1 + 2 * meta["history_size"], meta["conv_channels"],
-                         meta["num_residual_blocks"], meta["value_head_hidden_channels"], policy=meta["policy"],
-                         policy_sharpness=meta["policy_sharpness"])
+    if meta["policy"] == "selfplay":
+        sd = selfplay_state_dict()
+    else:
+        sd = live_state_dict(meta["seed"], 1 + 2 * meta["history_size"], meta["conv_channels"],
+                             meta["num_residual_blocks"], meta["value_head_hidden_channels"], policy=meta["policy"],
+                             policy_sharpness=meta["policy_sharpness"])
     assert weights_checksum(sd) == meta["weights_sha256_16"], "live_state_dict no longer reproduces the golden's weights"
     x = real_features(meta["boards"], meta["history_size"], meta["planes_seed"])
     assert planes_checksum(x) == meta["planes_sha256_16"]
@@ -79,7 +82,8 @@ def live_case(name: str):
     return meta, sd, x, {"policy": g[f"{name}_policy"], "value": g[f"{name}_value"]}
 
 
-LIVE_CASES = ["live_c128b9_h8_r1027", "frontier_c128b9_h8_r1027", "live_c256b19_h8_r1025"]
+LIVE_CASES = ["live_c128b9_h8_r1027", "frontier_c128b9_h8_r1027", "selfplay_c128b9_h8_r1027",
+              "live_c256b19_h8_r1025"]
 
 
 def load_cases() -> list[dict]:

@@ -78,6 +78,18 @@ def test_deep_tree_net_has_peaked_priors_and_a_live_value(positions):
     assert mass.mean() >= 0.6, mass.mean()  # most prior mass on legal moves, like a trained net
 
 
+def test_selfplay_trained_net_is_trained_like(positions):
+    """The deep_tree record's default net (bench_nets/, trained by
+    tools/selfplay_train.py): priors on legal moves like a trained net's, a
+    value spread over [-1, 1]."""
+    x, legal = positions
+    sd = bench.bench_state_dict("selfplay", 0, 17, 128, 9, 128)
+    p, v = _outputs(sd, x)
+    assert v.std() >= 0.3
+    assert (p * legal).sum(1).mean() >= 0.95
+    assert 0.3 <= p.max(1).mean() <= 0.5
+
+
 def test_torch_default_init_is_degenerate(positions):
     """Why the bench moved off it: constant value, (near-)uniform priors."""
     x, _ = positions

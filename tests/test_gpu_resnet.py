@@ -95,7 +95,8 @@ LIVE_TOL = {("bf16", 128): (5e-3, 1e-1, 2.5e-2), ("fp16", 128): (1e-3, 2e-2, 5e-
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
-@pytest.mark.parametrize("name", ["live_c128b9_h8_r1027", "frontier_c128b9_h8_r1027", "live_c256b19_h8_r1025"])
+@pytest.mark.parametrize("name", ["live_c128b9_h8_r1027", "frontier_c128b9_h8_r1027", "selfplay_c128b9_h8_r1027",
+                                  "live_c256b19_h8_r1025"])
 def test_live_nets_vs_reference_golden(om, name, dtype):
     """The nets bench.py runs (live value heads, the deep_tree
     net's peaked priors) against the reference's own AlphaZeroNet on >= 1025
