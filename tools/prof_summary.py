@@ -144,7 +144,7 @@ def nn_summary(outdir: str, prefix: str, tag: str) -> dict:
             for ln in log.read_text().splitlines():
                 if ln.startswith("k_resnet "):
                     line = ln
-    m = re.match(r"k_resnet (\d+)x(\d+)b (\w+): .*\(rows=(\d+)\)", line)
+    m = re.match(r"k_resnet (\d+)x(\d+)b (\w+)[^:]*: .*\(rows=(\d+)\)", line)
     rows = fpr = None
     if m:
         C, blocks, rows = int(m.group(1)), int(m.group(2)), int(m.group(4))
