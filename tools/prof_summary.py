@@ -44,7 +44,7 @@ def flops_per_row(C: int, R: int, in_ch: int = 17, hidden: int | None = None) ->
 
 def kernel_name_of(name: str) -> str:
     """k_resnet_w8<...> / k_tree(...) -> k_resnet_w8 / k_tree."""
-    return re.split(r"[<(]", name.strip(), maxsplit=1)[0].split()[-1]
+    return re.split(r"[<(]", name.strip(), maxsplit=1)[0].split()[-1].split("::")[-1]
 
 
 def gather(dirs: list[str], kernel: str = "k_resnet", regular_only: bool = True):
