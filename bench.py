@@ -332,6 +332,9 @@ def parse_args(argv: list[str]):
                     help="fewest extra rounds of the adaptive count (the margin over the cuts used)")
     ap.add_argument("--fixed-extra-rounds", action="store_true",
                     help="always --chain-cuts extra rounds (no adaptive count)")
+    ap.add_argument("--lockstep-moves", action="store_true",
+                    help="the multi-move call in lock step (every game waits for the group's slowest at each move, "
+                         "chain-splitting extra rounds) instead of free-running games (oamd_engine_set_free_running)")
     ap.add_argument("--extra-grid", type=int, default=128,
                     help="workgroups of the extra rounds' ResNet launches (0 = the regular grid)")
     ap.add_argument("--cpu-baseline-moves", type=int, default=24,
@@ -479,6 +482,7 @@ class EngineWorkload:
         self.b.engine.set_chain_split(args.chain_budget, args.chain_cuts)
         self.b.engine.set_extra_round_grid(args.extra_grid)
         self.b.engine.set_adaptive_extra_rounds(not args.fixed_extra_rounds, args.adaptive_min)
+        self.b.engine.set_free_running(not args.lockstep_moves)
         props = torch.cuda.get_device_properties(local)
         self.device_id = f"{os.uname().nodename}:{getattr(props, 'uuid', local)}"
 
@@ -652,7 +656,9 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
                                      if not args.fixed_extra_rounds else
                                      f"<= {args.chain_cuts} times per search"),
             "calls": ("search + selfplay_move per step" if args.per_move_calls or args.sync_search
-                      else f"one selfplay_steps call for the {args.steps} timed steps"),
+                      else f"one selfplay_steps call for the {args.steps} timed steps"
+                      + (", games in lock step (extra rounds)" if args.lockstep_moves else
+                         ", free-running games (each game's move runs in the round its search completes)")),
         },
     }
     if args.dry_run:

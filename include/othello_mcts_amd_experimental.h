@@ -69,6 +69,17 @@ int oamd_debug_read_stamps(uint64_t *out, int64_t n);
  * OAMD_INVALID_ARGUMENT. */
 int oamd_debug_tree_stamps(uint64_t *out, int64_t n, int32_t reset);
 
+/* Free-running self-play in oamd_engine_selfplay_steps (default on): every
+ * game plays its moves on its own — the round that completes a game's search
+ * also runs its move and its next search's first round — so no game waits at
+ * a move for the group's slowest one, and no extra rounds are run. Per game
+ * the operations and their order are those of n x (oamd_engine_search +
+ * oamd_engine_selfplay_move), and every output is identical; enable = 0 gives
+ * the lock-step multi-move call (searches with chain-splitting extra rounds).
+ * One game with num_threads > 1 (the thread-split schedule) is always
+ * lock-step. */
+int oamd_engine_set_free_running(oamd_engine *e, int32_t enable);
+
 #ifdef __cplusplus
 }
 #endif

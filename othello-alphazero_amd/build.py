@@ -31,8 +31,13 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", str(CSRC
 # tree.hip / rng.h / capi.hip tables must reproduce the reference's float
 # arithmetic bit for bit: no FMA contraction, IEEE division and sqrt.
 EXACT = ["-ffp-contract=off", "-fno-fast-math"]
+# tree.hip's kernels read statistics, links and game state that the same wave
+# has just written with vector stores (ordered by a wavefront fence, tree.hip
+# wave_order): no global load may go through the scalar cache, which does not
+# see those stores (tests/test_cpu_host.py checks the ISA)
+NO_SCALAR_LOADS = ["-mllvm", "-amdgpu-scalarize-global-loads=false"]
 UNITS = {
-    "tree.hip": EXACT,
+    "tree.hip": EXACT + NO_SCALAR_LOADS,
     "capi.hip": EXACT,
     # accumulators and fragments in arch VGPRs: the default heuristic parks the
     # 128 accumulators of a 1-wave/SIMD tile in AGPRs and shuffles them per MFMA;

@@ -226,6 +226,41 @@ struct oamd_engine {
         cuts_dev = dev;
         return OAMD_OK;
     }
+    // free-running self-play (oamd_engine_selfplay_steps, tree.hip k_tree_free):
+    // games play their moves without waiting for each other; the host enqueues
+    // rounds until every group's remaining-games counter (read back two chunks
+    // late, pinned memory behind events) is 0
+    bool free_running = true;
+    static constexpr int kFreeSlots = 4;
+    static constexpr int kFreeTailRounds = 4;
+    int32_t* remaining_dev = nullptr;   // [kMaxPipeline]
+    int32_t* remaining_host = nullptr;  // [kFreeSlots][kMaxPipeline], pinned
+    hipEvent_t free_ev[kFreeSlots][kMaxPipeline] = {};
+    int ensure_free_slots() {
+        if (remaining_dev) return OAMD_OK;
+        int32_t* dev = nullptr;
+        int32_t* host = nullptr;
+        hipEvent_t evs[kFreeSlots][kMaxPipeline] = {};
+        int rc = dalloc(&dev, (size_t)kMaxPipeline);
+        if (!rc && hipHostMalloc((void**)&host, sizeof(int32_t) * kFreeSlots * kMaxPipeline) != hipSuccess)
+            rc = fail(OAMD_RUNTIME, "free-running slots: hipHostMalloc failed");
+        for (auto& row : evs)
+            for (auto& x : row)
+                if (!rc && hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
+                    rc = fail(OAMD_RUNTIME, "free-running slots: hipEventCreate failed");
+        if (rc) {
+            for (auto& row : evs)
+                for (auto x : row)
+                    if (x) (void)hipEventDestroy(x);
+            if (host) (void)hipHostFree(host);
+            dfree(dev);
+            return rc;
+        }
+        remaining_host = host;
+        std::memcpy(free_ev, evs, sizeof(evs));
+        remaining_dev = dev;
+        return OAMD_OK;
+    }
     // workgroups of an extra round's ResNet launch (0 = the regular grid)
     int extra_grid = 128;
     int step_phase = 0;  // 1 = a selected round awaits its backup (step API)
@@ -518,6 +553,13 @@ struct oamd_engine {
             dfree(cuts_dev);
             (void)hipHostFree(cuts_host);
             for (auto& row : cuts_ev)
+                for (auto x : row) (void)hipEventDestroy(x);
+        }
+        if (remaining_dev) {
+            (void)hipDeviceSynchronize();  // no copy into remaining_host in flight
+            dfree(remaining_dev);
+            (void)hipHostFree(remaining_host);
+            for (auto& row : free_ev)
                 for (auto x : row) (void)hipEventDestroy(x);
         }
         for (int k = 0; k < n_pipe_streams; ++k) {
@@ -1210,6 +1252,25 @@ static void timing_end(oamd_engine* e, int steps, int NB, bool split, const Grou
     e->ev_cur ^= 1;
 }
 
+// Timing of R free-running rounds (every round has NN launches, none is a
+// backup-only final round)
+static void timing_end_rounds(oamd_engine* e, int R, const GroupPlan& P) {
+    const int pool = e->ev_cur;
+    e->ev_blocks[pool] = R * P.K;
+    e->ev_final[pool] = R * P.K;
+    e->ev_K[pool] = P.K;
+    e->ev_nn_groups[pool] = P.K;
+    int64_t nl = 0, rows = 0;
+    for (int k = 0; k < P.K; ++k) {
+        const int grows = P.ng[k] * e->L(), cb = e->nn_batch > 0 ? e->nn_batch : grows;
+        nl += (grows + cb - 1) / cb;
+        rows += grows;
+    }
+    e->ev_launches[pool] = (int64_t)R * nl;
+    e->ev_rows[pool] = (int64_t)R * rows;
+    e->ev_cur ^= 1;
+}
+
 // The rounds of one native search over the groups of P, enqueued on the group
 // streams (already forked from the engine stream). chained: the groups'
 // streams carry on from a previous search of the same call (a multi-move
@@ -1585,6 +1646,117 @@ int oamd_engine_selfplay_move(oamd_engine* e, const oamd_selfplay_config* cfg, i
     return OAMD_OK;
 }
 
+// Free-running self-play: n_moves moves of every game, each game on its own
+// (tree.hip k_tree_free). Rounds are enqueued in chunks: one per move's worth
+// of rounds (steps + 1 for the first search, steps for each later one: no game
+// can finish sooner), then tail chunks of kFreeTailRounds rounds until the
+// group's remaining-games counter, copied to pinned memory after every chunk
+// and read two chunks late (so the read never drains the queue), is 0. The
+// tail chunks' ResNet launches use the small looping grid (extra_grid): only
+// lagging games have rows then. Returns once the last chunk is enqueued.
+static int selfplay_steps_free(oamd_engine* e, oamd_net* net, const oamd_selfplay_config* cfg, int n_moves,
+                               int per_move, int32_t* actions, int32_t* finished, float* feat, float* pol) {
+    if (int rc = e->ensure_free_slots()) return rc;
+    GroupPlan P = plan_groups(e);
+    const int K = P.K, L = e->L();
+    const int T = e->cfg.num_threads, B = e->cfg.batch_size;
+    const int steps = (e->cfg.num_simulations + L - 1) / L;
+    const EngineView E = e->view();
+    const NetView N = net->view();
+    const SelfplayParams sp{cfg->temperature_moves, cfg->temperature, cfg->opening_moves, cfg->emit_targets};
+    const int budget = e->exact_interleaving && e->chain_budget > 0 ? e->chain_budget : 0;
+    const int nch = e->nn_chains < K ? e->nn_chains : K;
+    const int nlg = launches_per_group_round(e, P);
+    if (int rc = fork_groups(e, P)) return rc;
+    for (int k = 0; k < K; ++k) {
+        HIPCHK(hipMemsetAsync(e->rowcount + 2 * k, 0, 2 * sizeof(int32_t), P.st[k]));
+        HIPCHK(hipMemsetAsync(e->remaining_dev + k, 0, sizeof(int32_t), P.st[k]));
+        launch_free_begin(E, P.g0[k], P.ng[k], n_moves, e->remaining_dev + k, actions, finished, per_move, P.st[k]);
+    }
+    bool gdone[kMaxPipeline] = {};
+    const int64_t base_rounds = n_moves > 0 ? (int64_t)n_moves * steps + 1 : 0;
+    // a round completes at least one batch of every game still playing (or
+    // its move): a generous bound that only a kernel fault could exceed
+    const int64_t max_rounds = base_rounds + (int64_t)n_moves * ((int64_t)T * steps + 2) + 4 * oamd_engine::kFreeTailRounds;
+    int64_t round = 0;
+    for (int64_t chunk = 0; n_moves > 0; ++chunk) {
+        int R;
+        const bool tail = round >= base_rounds;
+        if (!tail) {
+            R = (int)std::min<int64_t>(round == 0 ? steps + 1 : steps, base_rounds - round);
+        } else {
+            if (chunk >= 2) {  // chunk - 2's readback: done by now while chunk - 1 is queued
+                const int slot = (int)((chunk - 2) % oamd_engine::kFreeSlots);
+                for (int k = 0; k < K; ++k) {
+                    if (gdone[k]) continue;
+                    HIPCHK(hipEventSynchronize(e->free_ev[slot][k]));
+                    if (e->remaining_host[slot * kMaxPipeline + k] == 0) gdone[k] = true;
+                }
+            }
+            bool all = true;
+            for (int k = 0; k < K; ++k) all = all && gdone[k];
+            if (all) break;
+            if (round >= max_rounds) return fail(OAMD_RUNTIME, "free-running self-play did not finish");
+            R = oamd_engine::kFreeTailRounds;
+        }
+        bool timed = false;
+        if (!tail) {
+            if (int rc = timing_begin(e, R, K, &timed)) return rc;
+        }
+        const int pool = e->ev_cur;
+        unsigned long long* span = nullptr;
+        if (int rc = e->reserve_spans((int64_t)K * R * nlg, &span)) return rc;
+        for (int s = 0; s < R; ++s) {
+            const int64_t r = round + s;
+            for (int k = 0; k < K; ++k) {
+                if (gdone[k]) continue;
+                hipStream_t sk = P.st[k];
+                hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
+                int* cnt = e->rowcount + 2 * k;
+                if (ev) HIPCHK(hipEventRecord(ev[0], sk));
+                launch_tree_free(E, sk, P.g0[k], P.ng[k], B, cnt + (r & 1), cnt + ((r + 1) & 1), budget, timed, sp,
+                                 n_moves, per_move, actions, finished, feat, pol, e->remaining_dev + k);
+                if (ev) HIPCHK(hipEventRecord(ev[1], sk));
+                if (K > 1 && (r > 0 || k >= nch)) HIPCHK(hipStreamWaitEvent(sk, e->nn_token[k % nch], 0));
+                if (ev) HIPCHK(hipEventRecord(ev[2], sk));
+                const int grows = P.ng[k] * L;
+                const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
+                const size_t r0 = (size_t)P.g0[k] * L;
+                for (int rr = 0, j = 0; rr < grows; rr += cb, ++j)
+                    launch_resnet_packed(N, E.feat, E.FW, E.H, std::min(cb, grows - rr), E.policy, E.value, sk,
+                                         E.rowlist + r0 + rr, cnt + (r & 1), rr,
+                                         span ? span + (size_t)2 * ((k * R + s) * nlg + j) : nullptr,
+                                         tail ? e->extra_grid : 0);
+                if (ev) HIPCHK(hipEventRecord(ev[3], sk));
+                if (K > 1) HIPCHK(hipEventRecord(e->nn_token[k % nch], sk));
+            }
+        }
+        const int slot = (int)(chunk % oamd_engine::kFreeSlots);
+        for (int k = 0; k < K; ++k) {
+            if (gdone[k]) continue;
+            HIPCHK(hipMemcpyAsync(e->remaining_host + slot * kMaxPipeline + k, e->remaining_dev + k, sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, P.st[k]));
+            HIPCHK(hipEventRecord(e->free_ev[slot][k], P.st[k]));
+        }
+        if (timed) timing_end_rounds(e, R, P);
+        round += R;
+    }
+    // the next search (or call) starts with empty evaluation lists
+    for (int k = 0; k < K; ++k) HIPCHK(hipMemsetAsync(e->rowcount + 2 * k, 0, 2 * sizeof(int32_t), P.st[k]));
+    e->grouped_searches += n_moves;
+    e->grouped_rounds += round;
+    LAUNCHCHK();
+    if (int rc = join_groups(e, P)) return rc;
+    e->step_phase = 0;
+    e->steps_left = 0;
+    return OAMD_OK;
+}
+
+int oamd_engine_set_free_running(oamd_engine* e, int32_t enable) {
+    e->free_running = enable != 0;
+    return OAMD_OK;
+}
+
 int oamd_engine_selfplay_steps(oamd_engine* e, oamd_net* net, const oamd_selfplay_config* cfg, int32_t n_moves,
                                int32_t per_move_outputs, int32_t* actions_dev, int32_t* finished_dev,
                                float* features_dev, float* policy_dev) {
@@ -1601,6 +1773,11 @@ int oamd_engine_selfplay_steps(oamd_engine* e, oamd_net* net, const oamd_selfpla
     GroupPlan P = plan_groups(e);
     const int T = e->cfg.num_threads;
     const bool split = G == 1 && P.K == 1 && T > 1 && T <= kMaxPipeline && e->tree_split();
+    if (!split && e->free_running) {
+        if (int rc = e->ensure_streams(P.K, P.K)) return rc;
+        return selfplay_steps_free(e, net, cfg, n_moves, per_move_outputs, actions_dev, finished_dev, features_dev,
+                                   policy_dev);
+    }
     if (split || P.K == 1) {  // one stream: the plain sequence of calls
         for (int i = 0; i < n_moves; ++i) {
             if (int rc = oamd_engine_search(e, net, nullptr, nullptr)) return rc;

@@ -47,7 +47,9 @@ struct GameState {
     int32_t ply;       // moves played since the last reset (self-play driver)
     int32_t resume;    // k_tree chain splitting: the virtual thread this game's next round starts at
     int32_t cuts;      // ... and the chains split so far in this search
-    int32_t pad[1];
+    int32_t moves_left;  // free-running self-play (k_tree_free): moves this game still plays in the call
+    int32_t fresh;       // ... 1: its next round starts a new search
+    int32_t pad[2];
 };
 
 // Packed NN input row (FW uint64 words): word 0 = meta, then (p1, p2) of the

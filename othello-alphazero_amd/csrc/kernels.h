@@ -42,6 +42,16 @@ void launch_self_play_data(const EngineView& E, int g, float* feat, float* pol, 
 void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int g0, int ng, int32_t* actions,
                           int32_t* finished, float* feat, float* pol, hipStream_t s);
 void launch_random_openings(const EngineView& E, int max_moves, uint64_t seed, hipStream_t s);
+// Free-running self-play (tree.hip k_tree_free): begin sets every game of the
+// group to play n_moves moves starting with a fresh search and counts them in
+// *remaining; each round runs one search round per game, a game's move in the
+// round its search completes, and its next search's first round after it.
+// *remaining must be zeroed before begin (stream order).
+void launch_free_begin(const EngineView& E, int g0, int ng, int n_moves, int32_t* remaining, int32_t* actions,
+                       int32_t* finished, int per_move, hipStream_t s);
+void launch_tree_free(const EngineView& E, hipStream_t s, int g0, int ng, int B, int* cnt_add, int* cnt_reset,
+                      int budget, bool timed, const SelfplayParams& sp, int n_moves, int per_move, int32_t* actions,
+                      int32_t* finished, float* feat, float* pol, int32_t* remaining);
 void launch_status(const EngineView& E, int32_t* out, hipStream_t s);
 void launch_legal_moves(const uint64_t* me, const uint64_t* opp, uint64_t* out, int64_t n,
                         hipStream_t s);

@@ -686,6 +686,8 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
             check(oamd_engine_round_counts(e.h, &searches, &rounds, &finals));
             return py::make_tuple(searches, rounds, finals);
         })
+        .def("set_free_running",
+             [](Engine& e, bool enable) { check(oamd_engine_set_free_running(e.h, enable ? 1 : 0)); })
         .def("set_exact_interleaving",
              [](Engine& e, bool enable) { check(oamd_engine_set_exact_interleaving(e.h, enable ? 1 : 0)); })
         .def("nn_timing", [](Engine& e) {

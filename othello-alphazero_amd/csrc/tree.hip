@@ -541,6 +541,107 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
 // only the round boundaries move. Each cut delays the game's remaining visits
 // by at most one round, so the host runs max_cuts extra rounds. budget = 0:
 // rounds always start at thread 0 (the step API and the single-game split).
+// Per-wave work counters of one k_tree launch.
+struct RoundAcc {
+    unsigned long long sims = 0, evals = 0, depth_sum = 0;
+    int depth_max = 0;
+};
+
+// One round of game g's search schedule (see k_tree): virtual threads
+// [t0, t1) visited cyclically from rp, each backing up its pending batch and
+// selecting its next ones (chain splitting after `budget` re-selections, at
+// most `max_cuts` cuts per search; cut_at = the thread whose chain stopped).
+// Returns true when the search is complete after this round: every thread
+// selected its `steps` batches and none waits for the NN (the reference's
+// search has returned, mcts.h:252-255).
+__device__ __forceinline__ bool search_round(const EngineView& E, int g, GameState* gs, size_t base, int t0,
+                                             int t1, int B, bool do_backup, bool do_select, bool fresh, int rp,
+                                             int budget, int max_cuts, int& cuts, bool& over, int& cut_at,
+                                             uint64_t& event, int hist_node, int hist_n, int& count,
+                                             bool& overflow, int* cnt_add, int list_base, RoundAcc& acc) {
+    const int lane = lane_id();
+    const int nt = t1 - t0;
+    int chain = 0;  // re-selections after all-terminal batches in this round
+    bool done = true;
+    // a search's first round starts every thread fresh, also the ones a split
+    // chain keeps it from visiting (their state is read from the next round on)
+    // (strided: a search may run up to 1024 virtual threads)
+    if (fresh && budget > 0)
+        for (int t = t0 + lane; t < t1; t += 64) E.tstate[(size_t)g * E.L + t] = 0;
+    for (int k = 0; k < nt && cut_at < 0; ++k) {
+        const int t = t0 + (rp - t0 + k) % nt;
+        // virtual thread t: batches selected so far in this search, and whether
+        // its last batch waits for the NN (a search's first round starts fresh)
+        int* ts = E.tstate + (size_t)g * E.L + t;
+        const int st = fresh ? 0 : *ts;
+        int sel = st & kTstateSel;
+        bool pend = (st & kTstatePend) != 0;
+        if (do_backup && pend) {
+            backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
+            pend = false;
+        }
+        // the thread's next batch; one whose leaves are all terminal needs no NN
+        // round trip (search_thread.cpp:102) and is backed up at once (:116-127),
+        // then the thread selects again, up to `steps` batches per search
+        bool again = false;  // the last batch was all terminal and is backed up
+        while (do_select && !pend && sel < E.steps) {
+            if (again && budget > 0 && chain >= budget) {
+                if (cuts < max_cuts) {
+                    cut_at = t;  // the next round continues this chain
+                    ++cuts;
+                    break;
+                }
+                over = true;  // no cut left: the chain runs on in this round
+            }
+            const unsigned long long ev0 = acc.evals;
+            TS_T(tsel0);
+            select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, acc.sims, acc.evals, cnt_add,
+                         list_base, acc.depth_sum, acc.depth_max);
+            TS_T(tsel1);
+            TS_ADD(kTsSelect, tsel1 - tsel0);
+            TS_ADD(kTsBatches, 1);
+            ++sel;
+            if (acc.evals != ev0 || !E.terminal_skip) {
+                pend = true;
+            } else {
+                backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
+                again = true;
+                ++chain;
+#if OAMD_CHAIN_PRIO > 0
+                // an all-terminal chain holds its pipeline group's round (and so
+                // its NN launch): from its first re-selection on, this wave
+                // issues ahead of the other group's ResNet waves (priority 1)
+                if (chain == 1) __builtin_amdgcn_s_setprio(OAMD_CHAIN_PRIO);
+#endif
+            }
+        }
+        if (lane == 0) *ts = sel | (pend ? kTstatePend : 0);
+        done = done && sel >= E.steps && !pend;
+    }
+    return done && cut_at < 0;
+}
+
+// The wave's work counters (lane 0): [0..1] this search (reset when a caller
+// asks for them), [2..3] cumulative since the engine was created
+// (oamd_engine_work_counters), [4..5] the searches that record timing events,
+// [6] descent depths summed over every selected leaf, [7] the deepest descent
+// (levels below the root; oamd_engine_descent_depths)
+__device__ __forceinline__ void add_counters(const EngineView& E, const RoundAcc& acc, bool timed) {
+    if (!E.counters) return;
+    atomicAdd(E.counters + 0, acc.sims);
+    atomicAdd(E.counters + 1, acc.evals);
+    atomicAdd(E.counters + 2, acc.sims);
+    atomicAdd(E.counters + 3, acc.evals);
+    if (timed) {
+        atomicAdd(E.counters + 4, acc.sims);
+        atomicAdd(E.counters + 5, acc.evals);
+    }
+    if (acc.sims) {
+        atomicAdd(E.counters + 6, acc.depth_sum);
+        atomicMax(E.counters + 7, (unsigned long long)acc.depth_max);
+    }
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree(EngineView E, int g0, int do_backup, int do_select,
                                              int t0, int t1, int B, int* cnt_add, int* cnt_reset, int fresh,
                                              int budget, int max_cuts, int timed, int* cuts_out) {
@@ -580,70 +681,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     uint64_t event = gs->event;
     const int hist_n = gs->hist_n;
     const int hist_node = lane < 16 ? gs->hist[lane] : -1;
-    unsigned long long sims = 0, evals = 0, depth_sum = 0;
-    int depth_max = 0;
+    RoundAcc acc;
     int count = gs->count;
     bool overflow = false;
-    const int nt = t1 - t0;
     const int rp = budget > 0 && !fresh ? gs->resume : t0;  // this round's first thread
     int cuts = budget > 0 && !fresh ? gs->cuts : 0;
-    int chain = 0;     // re-selections after all-terminal batches in this round
     bool over = false;  // a chain went past the budget with every cut used
-    int cut_at = -1;   // the thread whose chain this round stopped
-    // a search's first round starts every thread fresh, also the ones a split
-    // chain keeps it from visiting (their state is read from the next round on)
-    // (strided: a search may run up to 1024 virtual threads)
-    if (fresh && budget > 0)
-        for (int t = t0 + lane; t < t1; t += 64) E.tstate[(size_t)g * E.L + t] = 0;
-    for (int k = 0; k < nt && cut_at < 0; ++k) {
-        const int t = t0 + (rp - t0 + k) % nt;
-        // virtual thread t: batches selected so far in this search, and whether
-        // its last batch waits for the NN (a search's first round starts fresh)
-        int* ts = E.tstate + (size_t)g * E.L + t;
-        const int st = fresh ? 0 : *ts;
-        int sel = st & kTstateSel;
-        bool pend = (st & kTstatePend) != 0;
-        if (do_backup && pend) {
-            backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
-            pend = false;
-        }
-        // the thread's next batch; one whose leaves are all terminal needs no NN
-        // round trip (search_thread.cpp:102) and is backed up at once (:116-127),
-        // then the thread selects again, up to `steps` batches per search
-        bool again = false;  // the last batch was all terminal and is backed up
-        while (do_select && !pend && sel < E.steps) {
-            if (again && budget > 0 && chain >= budget) {
-                if (cuts < max_cuts) {
-                    cut_at = t;  // the next round continues this chain
-                    ++cuts;
-                    break;
-                }
-                over = true;  // no cut left: the chain runs on in this round
-            }
-            const unsigned long long ev0 = evals;
-            TS_T(tsel0);
-            select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, sims, evals, cnt_add,
-                         g0 * E.L, depth_sum, depth_max);
-            TS_T(tsel1);
-            TS_ADD(kTsSelect, tsel1 - tsel0);
-            TS_ADD(kTsBatches, 1);
-            ++sel;
-            if (evals != ev0 || !E.terminal_skip) {
-                pend = true;
-            } else {
-                backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
-                again = true;
-                ++chain;
-#if OAMD_CHAIN_PRIO > 0
-                // an all-terminal chain holds its pipeline group's round (and so
-                // its NN launch): from its first re-selection on, this wave
-                // issues ahead of the other group's ResNet waves (priority 1)
-                if (chain == 1) __builtin_amdgcn_s_setprio(OAMD_CHAIN_PRIO);
-#endif
-            }
-        }
-        if (lane == 0) *ts = sel | (pend ? kTstatePend : 0);
-    }
+    int cut_at = -1;    // the thread whose chain this round stopped
+    search_round(E, g, gs, base, t0, t1, B, do_backup != 0, do_select != 0, fresh != 0, rp, budget, max_cuts, cuts,
+                 over, cut_at, event, hist_node, hist_n, count, overflow, cnt_add, g0 * E.L, acc);
     if (lane == 0) {
         if (budget > 0) {
             gs->resume = cut_at >= 0 ? cut_at : rp;
@@ -671,24 +717,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
             }
         }
 #endif
-        if (E.counters && do_select) {
-            // [0..1] this search (reset when a caller asks for them), [2..3]
-            // cumulative since the engine was created (oamd_engine_work_counters)
-            atomicAdd(E.counters + 0, sims);
-            atomicAdd(E.counters + 1, evals);
-            atomicAdd(E.counters + 2, sims);
-            atomicAdd(E.counters + 3, evals);
-            if (timed) {  // [4..5] the searches that record timing events
-                atomicAdd(E.counters + 4, sims);
-                atomicAdd(E.counters + 5, evals);
-            }
-            // [6] descent depths summed over every selected leaf, [7] the
-            // deepest descent (levels below the root; oamd_engine_descent_depths)
-            if (sims) {
-                atomicAdd(E.counters + 6, depth_sum);
-                atomicMax(E.counters + 7, (unsigned long long)depth_max);
-            }
-        }
+        if (do_select) add_counters(E, acc, timed != 0);
     }
 }
 
@@ -958,19 +987,13 @@ __global__ void k_random_openings(EngineView E, int max_moves, uint64_t seed) {
 
 constexpr int kFinNoTargets = 4, kFinOverflow = 8;
 
-__global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayParams sp, int g0,
-                                                      int32_t* actions, int32_t* finished,
-                                                      float* feat_out, float* pol_out) {
-    const int g = g0 + (int)blockIdx.x;
+// One self-play move of game g (one wave): outputs at index g of the given
+// per-move slices.
+__device__ __forceinline__ void selfplay_move_game(const EngineView& E, const SelfplayParams& sp, int g,
+                                                   int32_t* actions, int32_t* finished, float* feat_out,
+                                                   float* pol_out) {
     const int lane = lane_id();
     GameState* gs = E.games + g;
-    if (!(gs->flags & kActive)) {
-        if (lane == 0) {
-            if (actions) actions[g] = -1;
-            if (finished) finished[g] = 0;
-        }
-        return;
-    }
     const size_t base = (size_t)g * E.cap;
     const int root = gs->root;
     const NodeLink lk = load_link(E.link + base + root);
@@ -1053,6 +1076,120 @@ __global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayPara
     }
 }
 
+__global__ __launch_bounds__(64) void k_selfplay_move(EngineView E, SelfplayParams sp, int g0,
+                                                      int32_t* actions, int32_t* finished,
+                                                      float* feat_out, float* pol_out) {
+    const int g = g0 + (int)blockIdx.x;
+    const int lane = lane_id();
+    GameState* gs = E.games + g;
+    if (!(gs->flags & kActive)) {
+        if (lane == 0) {
+            if (actions) actions[g] = -1;
+            if (finished) finished[g] = 0;
+        }
+        return;
+    }
+    selfplay_move_game(E, sp, g, actions, finished, feat_out, pol_out);
+}
+
+// ---------------------------------------------------------------------------
+// Free-running self-play (oamd_engine_selfplay_steps, capi.hip): every game
+// plays `n_moves` moves on its own; a round of this kernel is, per game, one
+// round of its current search (search_round) and, in the round that completes
+// the search, the move (selfplay_move_game: choice, 8-fold targets, apply,
+// restart) and the first round of its next search. Per game the operations
+// and their order are exactly those of n x (search + selfplay_move): the
+// rounds of one search, then its move, then the next search's rounds (a chain
+// cut only moves a round boundary, see k_tree). But no game waits for the
+// others at a move: a game whose search needs more rounds (chains near its
+// end) lags by those rounds while the others go on, so the group's ResNet
+// launches stay full and no extra rounds are needed. The host enqueues rounds
+// until `remaining` (games of the group with moves left) reads 0.
+// ---------------------------------------------------------------------------
+__global__ void k_free_begin(EngineView E, int g0, int ng, int n_moves, int32_t* remaining, int32_t* actions,
+                             int32_t* finished, int per_move) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // *remaining zeroed by the caller
+    if (i >= ng) return;
+    const int g = g0 + i;
+    GameState* gs = E.games + g;
+    const bool active = (gs->flags & kActive) != 0 && n_moves > 0;
+    gs->moves_left = active ? n_moves : 0;
+    gs->fresh = 1;
+    if (active) atomicAdd(remaining, 1);
+    for (int m = 0; !active && m < (per_move ? n_moves : (n_moves > 0 ? 1 : 0)); ++m) {
+        if (actions) actions[(size_t)m * E.G + g] = -1;
+        if (finished) finished[(size_t)m * E.G + g] = 0;
+    }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree_free(
+    EngineView E, int g0, int B, int* cnt_add, int* cnt_reset, int budget, int timed, SelfplayParams sp, int n_moves,
+    int per_move, int32_t* actions, int32_t* finished, float* feat_out, float* pol_out, int32_t* remaining) {
+    const int g = g0 + (int)blockIdx.x;
+    const int lane = lane_id();
+    if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
+    GameState* gs = E.games + g;
+    const size_t base = (size_t)g * E.cap;
+    int moves = gs->moves_left;
+    if (moves <= 0) return;
+    const int T = E.L / B;
+    const bool fresh = gs->fresh != 0;
+    uint64_t event = gs->event;
+    int hist_n = gs->hist_n;
+    int hist_node = lane < 16 ? gs->hist[lane] : -1;
+    int count = gs->count;
+    bool overflow = false;
+    RoundAcc acc;
+    int rp = fresh || budget <= 0 ? 0 : gs->resume;
+    int cuts = fresh ? 0 : gs->cuts;
+    bool over = false;
+    int cut_at = -1;
+    // no extra rounds to budget for: a game may cut its chains any number of times
+    constexpr int kNoCap = 0x3FFFFFFF;
+    const bool done = search_round(E, g, gs, base, 0, T, B, true, true, fresh, rp, budget, kNoCap, cuts, over, cut_at,
+                                   event, hist_node, hist_n, count, overflow, cnt_add, g0 * E.L, acc);
+    if (done) {
+        // the search has returned: publish the wave's state, then the move
+        // (k_selfplay_move's), which reads it from memory
+        if (lane == 0) {
+            gs->event = event;
+            gs->count = count;
+            if (overflow) atomicOr(&gs->flags, (int)kOverflow);
+        }
+        overflow = false;
+        __builtin_amdgcn_wave_barrier();
+        wait_stores();
+        const size_t slot = per_move ? (size_t)(n_moves - moves) * E.G : 0;
+        const size_t C = 1 + 2 * (size_t)E.H;
+        selfplay_move_game(E, sp, g, actions ? actions + slot : nullptr, finished ? finished + slot : nullptr,
+                           feat_out ? feat_out + slot * 8 * C * 64 : nullptr, pol_out ? pol_out + slot * 8 * 65 : nullptr);
+        --moves;
+        __builtin_amdgcn_wave_barrier();
+        wait_stores();  // (a compiler barrier too: the reloads below see the move's stores)
+        event = gs->event;
+        hist_n = gs->hist_n;
+        hist_node = lane < 16 ? gs->hist[lane] : -1;
+        count = gs->count;
+        rp = 0;
+        cuts = 0;
+        cut_at = -1;
+        if (moves > 0)  // the next search's first round, in this same round
+            search_round(E, g, gs, base, 0, T, B, true, true, true, 0, budget, kNoCap, cuts, over, cut_at, event,
+                         hist_node, hist_n, count, overflow, cnt_add, g0 * E.L, acc);
+    }
+    if (lane == 0) {
+        gs->moves_left = moves;
+        gs->fresh = 0;
+        gs->resume = cut_at >= 0 ? cut_at : rp;
+        gs->cuts = cuts;
+        gs->event = event;
+        gs->count = count;
+        if (overflow) atomicOr(&gs->flags, (int)kOverflow);
+        if (moves == 0 && remaining) atomicSub(remaining, 1);
+        add_counters(E, acc, timed != 0);
+    }
+}
+
 // Games whose node pool overflowed / whose descent hit the depth cap (sticky
 // flags since the game's last reset).
 __global__ void k_status(EngineView E, int32_t* out) {
@@ -1131,6 +1268,19 @@ void launch_selfplay_move(const EngineView& E, const SelfplayParams& sp, int g0,
                           int32_t* finished, float* feat, float* pol, hipStream_t s) {
     if (ng > 0)
         hipLaunchKernelGGL(k_selfplay_move, dim3(ng), dim3(64), 0, s, E, sp, g0, actions, finished, feat, pol);
+}
+void launch_free_begin(const EngineView& E, int g0, int ng, int n_moves, int32_t* remaining, int32_t* actions,
+                       int32_t* finished, int per_move, hipStream_t s) {
+    if (ng > 0)
+        hipLaunchKernelGGL(k_free_begin, dim3(blocks_for(ng, 256)), dim3(256), 0, s, E, g0, ng, n_moves, remaining,
+                           actions, finished, per_move);
+}
+void launch_tree_free(const EngineView& E, hipStream_t s, int g0, int ng, int B, int* cnt_add, int* cnt_reset,
+                      int budget, bool timed, const SelfplayParams& sp, int n_moves, int per_move, int32_t* actions,
+                      int32_t* finished, float* feat, float* pol, int32_t* remaining) {
+    if (ng > 0 && B > 0 && E.L % B == 0)
+        hipLaunchKernelGGL(k_tree_free, dim3(ng), dim3(64), 0, s, E, g0, B, cnt_add, cnt_reset, budget, (int)timed, sp,
+                           n_moves, per_move, actions, finished, feat, pol, remaining);
 }
 void launch_status(const EngineView& E, int32_t* out, hipStream_t s) {
     hipLaunchKernelGGL(k_status, dim3(blocks_for(E.G, 64)), dim3(64), 0, s, E, out);

@@ -363,14 +363,20 @@ def test_k_tree_reads_no_written_state_through_the_scalar_cache(tmp_path):
     descent's loads with a wavefront fence, not a vmcnt(0) drain (tree.hip
     wave_order). That holds for VECTOR loads (a wave's vector memory
     operations reach the cache in order); a load the compiler turned into a
-    scalar s_load goes through the scalar cache, which does not see the wave's
-    vector stores. Check the gfx950 ISA of the built k_tree: every s_load reads
-    the kernel arguments (s[0:1]) or GameState.key / .event (offsets 0x10 /
-    0x18), which k_tree reads once before its own stores. A compiler that
-    scalarises a statistic or link load fails this test (build with
-    OAMD_EXTRA_FLAGS=-DOAMD_TREE_DRAIN, the drained ordering, until reviewed)."""
+    scalar s_load would go through the scalar cache, which does not see the
+    wave's vector stores. build.py compiles tree.hip with
+    -amdgpu-scalarize-global-loads=false, so no global load is scalarised;
+    the gfx950 ISA of the built kernels confirms it: every s_load of k_tree
+    reads the kernel arguments (one base register, offsets inside the
+    argument segment), and every s_load of k_tree_free (which reloads its
+    arguments into other registers) lies inside its argument segment."""
+    import importlib.util
     import subprocess
 
+    spec = importlib.util.spec_from_file_location("oamd_build", PKG / "build.py")
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert "-amdgpu-scalarize-global-loads=false" in b.UNITS["tree.hip"]
     llvm = "/opt/rocm/lib/llvm/bin"
     obj = PKG / "build" / "tree.hip.o"
     fat, co = tmp_path / "tree.fatbin", tmp_path / "tree.co"
@@ -380,14 +386,32 @@ def test_k_tree_reads_no_written_state_through_the_scalar_cache(tmp_path):
                     "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
     dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", "--no-show-raw-insn", str(co)], check=True,
                          capture_output=True, text=True).stdout
-    body, inside = [], False
+    notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", str(co)], check=True, capture_output=True,
+                           text=True).stdout
+    # the metadata map lists each kernel's keys in order: .kernarg_segment_size
+    # comes before .name
+    kernarg, size = {}, None
+    for ln in notes.splitlines():
+        if ".kernarg_segment_size:" in ln:
+            size = int(ln.split(":", 1)[1])
+        elif ".name:" in ln and size is not None:
+            kernarg[ln.split(":", 1)[1].strip()] = size
+            size = None
+    bodies, cur = {}, None
     for ln in dis.splitlines():
         if ln.endswith(">:"):
-            inside = "6k_tree" in ln
-        elif inside:
-            body.append(ln.strip())
-    assert len(body) > 1000, "k_tree not found in the disassembly"
-    scalar = [ln for ln in body if ln.startswith(("s_load", "s_buffer_load"))]
-    other = [ln for ln in scalar if not re.search(r",\s*s\[0:1\],", ln)]
-    offsets = {ln.rsplit(",", 1)[1].split("//")[0].strip() for ln in other}
-    assert offsets <= {"0x10", "0x18"}, other
+            cur = ln.split("<", 1)[1].rstrip(">:")
+            bodies[cur] = []
+        elif cur:
+            bodies[cur].append(ln.strip())
+    for key, single_base in (("6k_tree", True), ("11k_tree_free", False)):
+        sym = next(n for n in bodies if n.startswith(f"_ZN4oamd{key}E"))
+        body = bodies[sym]
+        assert len(body) > 1000, sym
+        loads = [ln for ln in body if ln.startswith(("s_load", "s_buffer_load"))]
+        assert loads, sym
+        bases = {re.search(r",\s*(s\[\d+:\d+\]),", ln).group(1) for ln in loads}
+        offsets = [int(ln.split("//")[0].split(",")[-1].strip(), 16) for ln in loads]
+        assert max(offsets) < kernarg[sym], (sym, hex(max(offsets)))
+        if single_base:
+            assert len(bases) == 1, bases

@@ -292,6 +292,55 @@ def test_selfplay_steps_equal_move_by_move(om, G, pipeline):
                     f"{n} moves identical to search + selfplay_move, {restarts} game ends")
 
 
+@pytest.mark.parametrize("keep_all", [True, False])
+def test_free_running_games_equal_lock_step(om, keep_all):
+    """Free-running self-play (tree.hip k_tree_free, the default of
+    selfplay_steps): a game's move runs in the round its search completes and
+    its next search starts there, so games near their end (all-terminal
+    chains, cut every 2 re-selections) lag the others by rounds. Per game the
+    operations are those of n x (search + selfplay_move): actions, finish
+    codes, 8-fold targets and the final trees equal the lock-step call's and
+    the move-by-move calls' bit for bit; games end and restart inside the call."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(33, 9, 128, 2, 64), device=0)
+    n, G = 14, 128
+
+    def engine(free=True):
+        b = om.BatchedMCTS(G, history_size=4, num_simulations=160, num_threads=2, batch_size=8, seed=7,
+                           node_capacity=1 << 16)
+        b.random_openings(50, seed=3)  # late games: chains, endings and restarts inside the call
+        b.engine.set_free_running(free)
+        return b
+
+    a, c, m = engine(True), engine(False), engine(True)
+    oa = a.selfplay_steps(net, n, temperature_moves=12, opening_moves=4, emit_targets=True, keep_all=keep_all)
+    oc = c.selfplay_steps(net, n, temperature_moves=12, opening_moves=4, emit_targets=True, keep_all=keep_all)
+    outs = []
+    for _ in range(n):
+        m.search(net, sync=False)
+        o = m.selfplay_move(temperature_moves=12, opening_moves=4, emit_targets=True)
+        outs.append({k: v.clone() for k, v in o.items()})
+    torch.cuda.synchronize()
+    om_ = {k: torch.stack([o[k] for o in outs]) if keep_all else outs[-1][k] for k in outs[0]}
+    for k in ("actions", "finished", "features", "policy"):
+        assert torch.equal(oa[k], oc[k]), k
+        assert torch.equal(oa[k], om_[k]), k
+    for x, y in ((a, c), (a, m)):
+        vx, qx = x.root_stats()
+        vy, qy = y.root_stats()
+        assert torch.equal(vx, vy) and torch.equal(qx, qy)
+    fins = oa["finished"] if keep_all else torch.stack([o["finished"] for o in outs])
+    restarts = int(((fins & 3) != 0).sum())
+    assert restarts > 0
+    sa, ra, _ = a.engine.round_counts()
+    sc, rc_, _ = c.engine.round_counts()
+    numerics.record(f"free-running games keep_all={keep_all}",
+                    f"{G} games x {n} moves identical to lock step and move-by-move; {restarts} game ends; "
+                    f"rounds per move free {ra / max(1, sa):.2f} vs lock step {rc_ / max(1, sc):.2f}")
+    assert a.engine.status() == (0, 0)
+
+
 def test_chain_split_keeps_every_game_identical(om):
     """Chain splitting (oamd_engine_set_chain_split): near a game's end a thread
     whose batches come back all terminal re-selects at once (the reference's
