@@ -410,6 +410,7 @@ def test_adaptive_extra_rounds(om, opening):
     runs = []
     for adaptive in (True, False):
         x = om.BatchedMCTS(256, **kw)
+        x.engine.set_free_running(False)  # the lock-step multi-move call runs the extra rounds
         x.engine.set_chain_split(4, 16)
         x.engine.set_adaptive_extra_rounds(adaptive, 0)
         x.random_openings(opening, seed=13)
