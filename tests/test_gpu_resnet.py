@@ -89,8 +89,9 @@ def test_throughput_geometry_vs_reference_golden(om, golden_dir, name, dtype):
 # max |dpolicy|, max |dvalue|, rms dvalue, per dtype and tower depth (19 / 39
 # convs; measured C=128 bf16 8e-4-2.5e-3 / 0.057-0.067 / 0.0135-0.014, fp16
 # 2.2e-4-3.3e-4 / 0.0074-0.0085 / 0.0017-0.0019; C=256 bf16 2.4e-3 / 0.114 /
-# 0.0247)
-LIVE_TOL = {("bf16", 128): (5e-3, 1e-1, 2.5e-2), ("fp16", 128): (1e-3, 2e-2, 5e-3),
+# 0.0247; the self-play trained net's priors reach 0.99, its bf16 policy error
+# 1.17e-2, value 0.025 / rms 0.0034)
+LIVE_TOL = {("bf16", 128): (2.5e-2, 1e-1, 2.5e-2), ("fp16", 128): (4e-3, 2e-2, 5e-3),
             ("bf16", 256): (5e-3, 2e-1, 4e-2), ("fp16", 256): (1e-3, 4e-2, 8e-3)}
 
 
