@@ -354,6 +354,8 @@ def parse_args(argv: list[str]):
     ap.add_argument("--deep-tree-moves", type=int, default=20,
                     help="moves of the deep_tree sub-record from fresh openings (then --sustained-moves more; "
                          "0 = skip it)")
+    ap.add_argument("--no-config-records", dest="config_records", action="store_false",
+                    help="skip the configs[3] / configs[4]-shard sub-records")
     ap.add_argument("--latency-moves", type=int, default=20,
                     help="moves per setting of the single-game latency sub-record (0 = skip it)")
     ap.add_argument("--sync-search", action="store_true", help="host waits for every search (diagnostic)")
@@ -670,6 +672,8 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
             result["sustained"] = sustained
         if args.deep_tree_moves > 0:
             result["deep_tree"] = deep_tree_record(args, wl, world, rank, backend, sims_per_search)
+        if args.config_records:
+            result["other_configs"] = config_records(args, wl, world, rank, backend)
         if args.latency_moves > 0 and rank == 0:
             result["latency"] = latency_record(args, wl)
     # the CPU baseline on rank 0 at every world size, after every timed region;
@@ -741,6 +745,49 @@ def deep_tree_record(args, wl, world: int, rank: int, backend: str, sims_per_sea
                    "every selected leaf; k_tree_hidden: step time within 5 % of the union of the ResNet launches' "
                    "busy intervals")
     del dw
+    return out
+
+
+def config_records(args, wl, world: int, rank: int, backend: str) -> dict:
+    """VERDICT r4 (What's weak 9): configs[3] (256x20b bf16, 1600 sims/move)
+    and the per-GPU shard of configs[4] (512 games, 128x10b fp16, eval batch
+    2048) in the driver's own line, on short windows after the headline's (the
+    same rank path; every rank runs its shard, so at N GPUs configs[4]'s
+    record is N x 512 games). Live seeded nets, like the headline's."""
+    import copy
+    import gc
+
+    if getattr(wl, "b", None) is not None:
+        del wl.b
+    gc.collect()
+    out = {}
+    specs = (("configs3", "256x20b ResNet bf16, 256 games per GPU, 1600 sims/move (BASELINE configs[3])",
+              dict(channels=256, blocks=20, hidden=256, sims=1600, dtype="bf16", eval_batch=0, games=256), 2, 4),
+             ("configs4_shard", "128x10b ResNet fp16, 512 games per GPU, eval batch 2048, 800 sims/move "
+              "(BASELINE configs[4]: 4096 games over 8 GPUs)",
+              dict(channels=128, blocks=10, hidden=128, sims=800, dtype="fp16", eval_batch=2048, games=512), 2, 10))
+    for name, desc, over, warm, n in specs:
+        a = copy.copy(args)
+        a.__dict__.update(over)
+        a.steps = n
+        w = EngineWorkload(a, rank, wl.local, net_kind="live")
+        w.steps(warm)
+        w.sync()
+        dt, own, m = run_window(a, w, world, backend, n)
+        L = a.threads * a.batch
+        sps = L * ((a.sims + L - 1) // L)
+        mf = measured_fields(a, m, "")
+        r = mf["roofline"]
+        out[name] = {"workload": desc, "steps": n, "warmup": warm,
+                     "value": round(aggregate_rate(world, a.games, sps, n, dt), 1), "unit": "simulations/s",
+                     "ms_per_step": round(dt * 1e3 / n, 3), "this_rank_ms": round(own * 1e3, 3),
+                     "dtype": a.dtype,
+                     "roofline": {k: r[k] for k in ("bound", "achieved", "peak", "unit", "frac", "busy_ms_per_launch",
+                                                    "rows_per_launch", "n_eval_per_launch", "flops_per_row",
+                                                    "timed_region_launches")},
+                     "work": mf["work"], "tree_kernels": mf["tree_kernels"]}
+        del w
+        gc.collect()
     return out
 
 

@@ -85,7 +85,7 @@ run_recipe() {
         for v in ${AB_ORDER:-$(ls abv)}; do
           cp abv/$v/liboamd.so $PKG/liboamd.so
           step 600 "$OUT/benchvar_${n}_${v}_$r.json" env OAMD_AB_VARIANT=$v python bench.py --cpu-baseline-moves 0 \
-            --deep-tree-moves 0 --latency-moves 0 "$@" || { restore_lib; return 1; }
+            --deep-tree-moves 0 --latency-moves 0 --no-config-records "$@" || { restore_lib; return 1; }
         done
       done
       restore_lib ;;
