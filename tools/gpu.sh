@@ -18,6 +18,14 @@
 #   stamps NAME VARIANT [VAR=val]  tools/nn_stamps.py with abv/VARIANT (built with -DOAMD_STAMPS)
 #   benchvar NAME [bench args]     bench line of every prebuilt variant, ROUNDS interleaved sweeps
 #   treestamps NAME [VAR=val]      tools/tree_stamps.py with abv/ts (tools/tree_stamps_build.sh)
+#   records                        the canonical record set: tests, the C2 bench line (20 + 5 steps), kernel
+#                                  traces of C2 / 200 steps / C4 / C5, the C2 line under torch.distributed.run
+#                                  (summary: tools/record_summary.py)
+#   benchpmc NAME                  the four PMC passes over the C2 bench (tools/prof_summary.py bench)
+#   nnpmcset NAME [VAR=val ...]    the four PMC passes over the standalone kernel (tools/prof_summary.py nn)
+# A/B sweeps are plain recipe lists, e.g. ROUNDS of
+#   bash tools/gpu.sh "bench a_1 ARGS_A" "bench b_1 ARGS_B" "bench a_2 ARGS_A" "bench b_2 ARGS_B"
+# (the round-4 one-off sweep scripts were folded into this form; their results are in profiles/r04/ab/).
 # Trace post-processing: tools/kt_gaps.py (gaps between ResNet launches), tools/round_profile.py
 # (a step split by round). Every step runs under its own time limit; the first failing step ends the run
 # (no retries). Summaries: python tools/prof_summary.py (in the build container).
@@ -89,6 +97,22 @@ run_recipe() {
         done
       done
       restore_lib ;;
+    records)
+      local C2="--steps 20 --warmup 5" C4="--sims 1600 --channels 256 --blocks 20 --hidden 256 --steps 4 --warmup 1"
+      local C5="--games 512 --dtype fp16 --eval-batch 2048 --steps 10 --warmup 2"
+      local Q="--sustained-moves 0 --cpu-baseline-moves 0 --deep-tree-moves 0 --latency-moves 0 --no-config-records"
+      run_recipe tests && run_recipe bench c2 $C2 && run_recipe trace c2 $C2 $Q &&
+        run_recipe trace s200 --steps 200 --warmup 5 $Q && run_recipe trace c4 $C4 $Q &&
+        run_recipe trace c5 $C5 $Q && run_recipe launch c2 $C2 $Q ;;
+    benchpmc) local n=$1
+      local A="--steps 20 --warmup 5 --sustained-moves 0 --cpu-baseline-moves 0 --deep-tree-moves 0 --latency-moves 0 --no-config-records"
+      run_recipe pmc ${n}_a SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_WAIT_INST_LDS,SQ_INSTS_MFMA,SQ_INSTS_LDS,SQ_INSTS_SALU $A &&
+        run_recipe pmc ${n}_b SQ_VALU_MFMA_BUSY_CYCLES,SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_INSTS_VALU,GRBM_GUI_ACTIVE $A &&
+        run_recipe pmc ${n}_c FETCH_SIZE $A && run_recipe pmc ${n}_d WRITE_SIZE,TCC_HIT_sum,TCC_MISS_sum $A ;;
+    nnpmcset) local p=$1; shift
+      run_recipe nnpmc ${p}_a SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_WAIT_INST_LDS,SQ_INSTS_MFMA,SQ_INSTS_LDS,SQ_INSTS_SALU "$@" &&
+        run_recipe nnpmc ${p}_b SQ_VALU_MFMA_BUSY_CYCLES,SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_INSTS_VALU,GRBM_GUI_ACTIVE "$@" &&
+        run_recipe nnpmc ${p}_c FETCH_SIZE "$@" && run_recipe nnpmc ${p}_d WRITE_SIZE,TCC_HIT_sum,TCC_MISS_sum "$@" ;;
     *) echo "unknown recipe: $recipe"; return 2 ;;
   esac
 }

@@ -5,7 +5,7 @@ one game with the fused native ResNet, as ``player.py``/``train.py`` use it.
 Prints one JSON line per setting: median / p90 ms per ``search`` over the
 moves of one game (argmax play), for self-play settings (800 sims, T=2 x B=16,
 eps=0.25) and evaluation settings (3200 sims, eps=0, README.md:195).
-Synthetic seeded 128x10b weights."""
+Seeded live 128x10b weights (the bench's)."""
 
 import json
 import sys
@@ -18,7 +18,7 @@ sys.path.insert(0, str(ROOT / "othello-alphazero_amd"))
 import torch  # noqa: E402
 
 import othello_mcts as om  # noqa: E402
-from othello_mcts.synthetic import alphazero_state_dict  # noqa: E402
+from othello_mcts.synthetic import live_state_dict  # noqa: E402
 
 
 def run(net, sims, eps, moves):
@@ -73,7 +73,7 @@ def breakdown(net, sims, moves, eps=0.25):
 
 
 def main():
-    net = om.NativeNet(alphazero_state_dict(1, 17, 128, 9, 128), device=0)
+    net = om.NativeNet(live_state_dict(2025, 17, 128, 9, 128), device=0)
     for sims, eps, moves in ((800, 0.25, 40), (3200, 0.0, 20)):
         print(json.dumps(run(net, sims, eps, moves)), flush=True)
     print(json.dumps(breakdown(net, 800, 20)), flush=True)

@@ -1,4 +1,4 @@
-"""Summarise a record set of tools/r04_records.sh (build container):
+"""Summarise a record set of tools/gpu.sh records (build container):
   python tools/record_summary.py gpurun_out/<N> <tag>
 writes profiles/<tag>_<config>_kernel_stats.csv / _resnet_busy.json (trace
 cross-checks) and prints the bench lines' headline, sustained and roofline
