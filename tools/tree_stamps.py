@@ -9,7 +9,7 @@ leaf's post-descent work (virtual loss, path, features) and per backed-up
 leaf, plus the longest wave of the move's rounds.
 Env: MOVES (default 64), GAMES (256), PIPE (pipeline groups; 1 = no
 co-resident ResNet launch of the other group: k_tree's uncontended speed),
-BUDGET / CUTS (chain splitting)."""
+BUDGET / CUTS (chain splitting), NET=torch-default (default: the live net)."""
 import ctypes
 import os
 import sys
@@ -22,7 +22,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import othello_mcts as om  # noqa: E402
-from othello_mcts.synthetic import alphazero_state_dict  # noqa: E402
+from othello_mcts.synthetic import alphazero_state_dict, live_state_dict  # noqa: E402
 
 NAMES = ["waves", "cycles", "descent", "levels", "leaves", "post", "backup", "backed_up", "terminal",
          "max_cycles", "batches", "select"]
@@ -38,8 +38,10 @@ def read(reset=1):
     return dict(zip(NAMES, np.frombuffer(buf, dtype=np.uint64).astype(np.int64).tolist()))
 
 
-net = om.NativeNet(alphazero_state_dict(2025, 17, 128, 9, 128), device=0)
-b = om.BatchedMCTS(games, history_size=8, num_simulations=800, num_threads=2, batch_size=16, seed=2025)
+net = om.NativeNet(alphazero_state_dict(2025, 17, 128, 9, 128) if os.environ.get("NET") == "torch-default"
+                   else live_state_dict(2025, 17, 128, 9, 128), device=0)
+b = om.BatchedMCTS(games, history_size=8, num_simulations=int(os.environ.get("SIMS", "800")), num_threads=2,
+                   batch_size=16, seed=2025, dirichlet_epsilon=float(os.environ.get("EPS", "0.25")))
 b.random_openings(8, seed=2025)
 if os.environ.get("PIPE"):
     b.engine.set_pipeline(int(os.environ["PIPE"]))

@@ -6,9 +6,10 @@ cd "$(dirname "$0")/.."
 CS=othello-alphazero_amd/csrc
 CXX="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -fno-gpu-rdc -I $CS -I include -DOAMD_TREE_STAMPS"
 EXACT="-ffp-contract=off -fno-fast-math"
+NOSCALAR="-mllvm -amdgpu-scalarize-global-loads=false"
 RF="-mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp"
 mkdir -p abv/ts
-$CXX $EXACT -c $CS/tree.hip -o abv/ts/tree.o &
+$CXX $EXACT $NOSCALAR -c $CS/tree.hip -o abv/ts/tree.o &
 $CXX $EXACT -c $CS/capi.hip -o abv/ts/capi.o &
 $CXX $RF -c $CS/resnet.hip -o abv/ts/resnet.o &
 wait
