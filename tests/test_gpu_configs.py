@@ -341,6 +341,31 @@ def test_free_running_games_equal_lock_step(om, keep_all):
     assert a.engine.status() == (0, 0)
 
 
+def test_free_running_at_the_benched_shape(om):
+    """configs[1] as bench.py runs it (256 games, 128x10b live net, 800 sims,
+    random openings, 24 moves in one multi-move call, games ending and
+    restarting inside it): free-running games give the lock-step call's
+    actions, finish codes and trees bit for bit."""
+    import bench
+
+    net = om.NativeNet(bench.bench_state_dict("live", 2025, 17, 128, 9, 128), device=0)
+    outs, trees = [], []
+    for free in (True, False):
+        b = om.BatchedMCTS(256, history_size=8, num_simulations=800, num_threads=2, batch_size=16, seed=2025)
+        b.random_openings(40, seed=7)  # late openings: endgames, chains and restarts inside the call
+        b.engine.set_free_running(free)
+        o = b.selfplay_steps(net, 24, temperature_moves=12, opening_moves=8, emit_targets=False)
+        torch.cuda.synchronize()
+        outs.append(o)
+        trees.append(b.root_stats())
+        assert b.engine.status() == (0, 0)
+    assert torch.equal(outs[0]["actions"], outs[1]["actions"]) and torch.equal(outs[0]["finished"], outs[1]["finished"])
+    assert torch.equal(trees[0][0], trees[1][0]) and torch.equal(trees[0][1], trees[1][1])
+    ends = int(((outs[0]["finished"] & 3) != 0).sum())
+    assert ends > 50
+    numerics.record("free-running games, configs[1] shape", f"256 games x 24 moves == lock step; {ends} game ends")
+
+
 def test_chain_split_keeps_every_game_identical(om):
     """Chain splitting (oamd_engine_set_chain_split): near a game's end a thread
     whose batches come back all terminal re-selects at once (the reference's
