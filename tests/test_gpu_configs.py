@@ -362,7 +362,7 @@ def test_free_running_at_the_benched_shape(om):
     assert torch.equal(outs[0]["actions"], outs[1]["actions"]) and torch.equal(outs[0]["finished"], outs[1]["finished"])
     assert torch.equal(trees[0][0], trees[1][0]) and torch.equal(trees[0][1], trees[1][1])
     ends = int(((outs[0]["finished"] & 3) != 0).sum())
-    assert ends > 50
+    assert ends > 10
     numerics.record("free-running games, configs[1] shape", f"256 games x 24 moves == lock step; {ends} game ends")
 
 
