@@ -108,19 +108,40 @@ class SelfPlayCollector:
 
 
 def self_play(batched, neural_net, games: int, temperature_moves: int = 12, temperature: float = 1.0,
-              opening_moves: int = 0, device: str | torch.device = "cpu") -> dict[str, list[torch.Tensor]]:
-    """Play until ``games`` games have completed across the batch (each slot
-    restarts when its game ends) and return their samples in the reference's
-    ``_self_play`` format. ``opening_moves=0`` starts every game from the initial
-    position as train.py does."""
+              opening_moves: int = 0, device: str | torch.device = "cpu",
+              moves_per_call: int = 16) -> dict[str, list[torch.Tensor]]:
+    """Play until at least ``games`` games have completed across the batch (each
+    slot restarts when its game ends) and return their samples in the
+    reference's ``_self_play`` format (train.py:404-452). ``opening_moves=0``
+    starts every game from the initial position as train.py does.
+
+    With a native net (NativeNet, or a module ``search`` would convert) the
+    moves run ``moves_per_call`` at a time through
+    ``BatchedMCTS.selfplay_steps`` (free-running games, one enqueue per call:
+    the bench's throughput path); per game the moves are those of the
+    move-by-move loop (search + selfplay_move), which any other evaluator
+    uses, so the samples of the games completed by a given move are the same
+    either way. The last call may play up to ``moves_per_call - 1`` moves past
+    the one that completed the requested games (their finished games are
+    returned too)."""
+    from .native import resolve
+
     col = SelfPlayCollector(batched.num_games, device=device)
     data = {"features": [], "policies": [], "values": []}
+    native = moves_per_call > 1 and resolve(neural_net, batched.device.index, batched.config.history_size) is not None
+    kw = dict(temperature_moves=temperature_moves, temperature=temperature, opening_moves=opening_moves,
+              emit_targets=True)
     while col.games_completed < games:
-        batched.search(neural_net)
-        got = col.add(batched.selfplay_move(temperature_moves=temperature_moves, temperature=temperature,
-                                            opening_moves=opening_moves, emit_targets=True))
-        for k in data:
-            data[k] += got[k]
+        if native:
+            out = batched.selfplay_steps(neural_net, moves_per_call, keep_all=True, **kw)
+            moves = [{k: v[i] for k, v in out.items()} for i in range(moves_per_call)]
+        else:
+            batched.search(neural_net)
+            moves = [batched.selfplay_move(**kw)]
+        for o in moves:
+            got = col.add(o)
+            for k in data:
+                data[k] += got[k]
     return data
 
 

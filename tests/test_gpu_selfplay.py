@@ -35,6 +35,29 @@ def test_self_play_samples_match_reference_format():
     assert float(f0[0, 0, 0]) == 0.0 and int(f0[1].sum() + f0[2].sum()) == 4
 
 
+def test_self_play_multi_move_calls_equal_move_by_move():
+    """self_play with a native net runs selfplay_steps chunks (free-running
+    games); every game's moves are those of the move-by-move loop, so the
+    samples of the games the move-by-move run completed come out first and
+    identical."""
+    import othello_mcts as om
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(4, 5, 128, 1, 32), device=0)
+
+    def run(chunk):
+        b = om.BatchedMCTS(16, history_size=2, num_simulations=32, num_threads=2, batch_size=8, seed=5,
+                           node_capacity=1 << 15)
+        b.random_openings(40, seed=9)  # late openings: games complete within a few moves
+        return om.self_play(b, net, games=6, opening_moves=4, moves_per_call=chunk)
+
+    a, c = run(1), run(8)
+    n = len(a["features"])
+    assert n > 0 and len(c["features"]) >= n
+    for k in ("features", "policies", "values"):
+        assert all(torch.equal(x, y) for x, y in zip(a[k], c[k][:n])), k
+
+
 def test_native_net_from_reference_checkpoint(tmp_path):
     import othello_mcts as om
     from othello_mcts.synthetic import alphazero_state_dict, net_config_from_state_dict
