@@ -292,6 +292,39 @@ def test_selfplay_steps_equal_move_by_move(om, G, pipeline):
                     f"{n} moves identical to search + selfplay_move, {restarts} game ends")
 
 
+@pytest.mark.parametrize("T,B,nn_batch,pipeline,exact", [(3, 8, 0, 0, True), (4, 4, 384, 3, True),
+                                                         (2, 16, 0, 0, False)])
+def test_free_running_schedules_equal_lock_step(om, T, B, nn_batch, pipeline, exact):
+    """Free-running games against the lock-step call for other schedules: 3 and
+    4 virtual threads, an NN evaluation batch of 384 rows over 3 pipeline
+    groups, round-robin endgames. Actions, finish codes, targets and trees."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(35, 9, 128, 2, 64), device=0)
+
+    def engine(free):
+        b = om.BatchedMCTS(96, history_size=4, num_simulations=120, num_threads=T, batch_size=B, seed=11,
+                           node_capacity=1 << 16)
+        b.random_openings(48, seed=13)
+        b.engine.set_free_running(free)
+        b.engine.set_nn_batch(nn_batch)
+        b.engine.set_pipeline(pipeline)
+        b.engine.set_exact_interleaving(exact)
+        return b
+
+    a, c = engine(True), engine(False)
+    oa = a.selfplay_steps(net, 10, temperature_moves=12, opening_moves=4, emit_targets=True)
+    oc = c.selfplay_steps(net, 10, temperature_moves=12, opening_moves=4, emit_targets=True)
+    torch.cuda.synchronize()
+    for k in ("actions", "finished", "features", "policy"):
+        assert torch.equal(oa[k], oc[k]), k
+    va, qa = a.root_stats()
+    vc, qc = c.root_stats()
+    assert torch.equal(va, vc) and torch.equal(qa, qc)
+    assert int(((oa["finished"] & 3) != 0).sum()) > 0
+    assert a.engine.status() == (0, 0)
+
+
 @pytest.mark.parametrize("keep_all", [True, False])
 def test_free_running_games_equal_lock_step(om, keep_all):
     """Free-running self-play (tree.hip k_tree_free, the default of
