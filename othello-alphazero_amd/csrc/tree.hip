@@ -95,6 +95,25 @@ __device__ __forceinline__ float wave_max(float v) {
     return wave_scan_last(v, -__builtin_inff(), [](float a, float b) { return fmaxf(a, b); });
 }
 
+// The same scans over the first n lanes only (lanes >= n hold the identity):
+// with n <= 16 (almost every node: Othello positions rarely have more legal
+// moves) row 0 holds them all, so the two row_bcast steps are skipped and the
+// total is read from lane 15.
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_scan_first_n(T v, T id, Op op, int n) {
+    static_assert(sizeof(T) == 4, "32-bit lanes");
+    T t = op(v, dpp_move<0x111, 0xF, 0xF>(v, id));  // row_shr:1
+    t = op(t, dpp_move<0x112, 0xF, 0xF>(v, id));    // row_shr:2
+    t = op(t, dpp_move<0x113, 0xF, 0xF>(v, id));    // row_shr:3
+    t = op(t, dpp_move<0x114, 0xF, 0xE>(t, id));    // row_shr:4, banks 1-3
+    t = op(t, dpp_move<0x118, 0xF, 0xC>(t, id));    // row_shr:8, banks 2-3
+    if (n > 16) {
+        t = op(t, dpp_move<0x142, 0xA, 0xF>(t, id));  // row_bcast:15 into rows 1, 3
+        t = op(t, dpp_move<0x143, 0xC, 0xF>(t, id));  // row_bcast:31 into rows 2, 3
+    }
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), n > 16 ? 63 : 15));
+}
+
 __device__ __forceinline__ int wave_max_i(int v) {
     return wave_scan_last(v, (int)0x80000000, [](int a, int b) { return a > b ? a : b; });
 }
@@ -104,6 +123,13 @@ __device__ __forceinline__ int wave_max_i(int v) {
 // Values are finite or -inf (no NaN).
 __device__ __forceinline__ int wave_argmax_first(float v, int) {
     const float m = wave_max(v);
+    const uint64_t eq = __ballot(v == m);
+    return __ffsll((unsigned long long)eq) - 1;
+}
+
+// ... over the first n lanes (the others hold -inf)
+__device__ __forceinline__ int wave_argmax_first_n(float v, int n) {
+    const float m = wave_scan_first_n(v, -__builtin_inff(), [](float a, float b) { return fmaxf(a, b); }, n);
     const uint64_t eq = __ballot(v == m);
     return __ffsll((unsigned long long)eq) - 1;
 }
@@ -290,7 +316,7 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
             int best = 0;
             if (nc > 1) {
                 const NodeStat cs{cs4.x, __int_as_float(cs4.y), __int_as_float(cs4.z), __int_as_float(cs4.w)};
-                const int total = wave_sum(lane < nc ? cs.n : 0);
+                const int total = wave_scan_first_n(lane < nc ? cs.n : 0, 0, [](int a, int b) { return a + b; }, nc);
                 const float mult = er * sqrt_count(E, total);
                 float prob = cs.p;
                 if (node == root && E.eps > 0.0f) {
@@ -307,7 +333,7 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
                 }
                 float ucb = cs.q + mult * prob / (1.0f + (float)cs.n);
                 if (lane >= nc) ucb = -__builtin_inff();
-                best = wave_argmax_first(ucb, lane);
+                best = wave_argmax_first_n(ucb, nc);
             }  // a single child is taken without scoring (search_thread.cpp:194-196)
             const int child = fc + best;
             const int4 clk4 = make_int4(readlane_i(cl4.x, best), readlane_i(cl4.y, best),

@@ -4,12 +4,12 @@ import json
 import sys
 from pathlib import Path
 
-for f in sorted(Path(sys.argv[1]).glob("bench_*.json")):
+for f in sorted(Path(sys.argv[1]).glob("bench*_*.json")):
     for ln in f.read_text().splitlines():
         if ln.startswith("{"):
             d = json.loads(ln)
             s = d.get("sustained", {})
-            print(f"{f.stem[6:]:14s} {d['value'] / 1e6:7.3f} M  frac {d['roofline']['frac']:.4f}  "
+            print(f"{f.stem.split('_', 1)[1]:14s} {d['value'] / 1e6:7.3f} M  frac {d['roofline']['frac']:.4f}  "
                   f"rounds {d['tree_kernels']['rounds_per_search']:7.3f} | sustained "
                   f"{s.get('value', 0) / 1e6:7.3f} M  frac {s.get('roofline', {}).get('frac', 0):.4f}  "
                   f"rounds {s.get('tree_kernels', {}).get('rounds_per_search', 0):7.3f}")

@@ -15,6 +15,7 @@ CS=othello-alphazero_amd/csrc
 RF="-mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp"
 CXX="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -fno-gpu-rdc"
 EXACT="-ffp-contract=off -fno-fast-math"
+NOSCALAR="-mllvm -amdgpu-scalarize-global-loads=false"  # as build.py builds tree.hip
 rm -rf abv
 IFS=';' read -ra SETS <<< "${VARIANTS:?}"
 pids=()
@@ -25,7 +26,7 @@ for e in "${SETS[@]}"; do
     set -e
     if [[ "${src:-}" == "+" ]]; then  # every unit of the working tree, built with the flags
       $CXX -I $CS -I include $flags $RF -c $CS/resnet.hip -o abv/$name/resnet.o
-      $CXX -I $CS -I include $flags $EXACT -c $CS/tree.hip -o abv/$name/tree.o
+      $CXX -I $CS -I include $flags $EXACT $NOSCALAR -c $CS/tree.hip -o abv/$name/tree.o
       $CXX -I $CS -I include $flags $EXACT -c $CS/capi.hip -o abv/$name/capi.o
       objs="abv/$name/tree.o abv/$name/capi.o"
     elif [[ "${src:-}" == @* ]]; then
@@ -33,7 +34,7 @@ for e in "${SETS[@]}"; do
       git archive "$rev" othello-alphazero_amd/csrc include | tar -x -C $d
       inc="-I $d/$CS -I $d/include"
       $CXX $inc $flags $RF -c $d/$CS/resnet.hip -o abv/$name/resnet.o
-      $CXX $inc $EXACT -c $d/$CS/tree.hip -o abv/$name/tree.o
+      $CXX $inc $EXACT $NOSCALAR -c $d/$CS/tree.hip -o abv/$name/tree.o
       $CXX $inc $EXACT -c $d/$CS/capi.hip -o abv/$name/capi.o
       objs="abv/$name/tree.o abv/$name/capi.o"
     else
