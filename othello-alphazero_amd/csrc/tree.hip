@@ -466,8 +466,9 @@ __device__ __forceinline__ int kth_square(uint64_t mask, int k) {
 
 // Expand position P (not terminal, legal != 0) into children fc .. fc+nc-1 in
 // legal_actions order (position.h:308-326), priors policy[transform(a, t)].
+// pol_l: entry `lane` of the leaf's policy row (prefetched by backup_range)
 __device__ __forceinline__ void expand_quads(const EngineView& E, size_t base, int leaf, const Pos& P, int fc,
-                                             int nc, int t, const float* pol) {
+                                             int nc, int t, float pol_l) {
     const int lane = lane_id();
     const int q = lane & 3;
     const int mag = q == 0 ? 1 : (q == 1 ? 7 : (q == 2 ? 8 : 9));
@@ -495,6 +496,8 @@ __device__ __forceinline__ void expand_quads(const EngineView& E, size_t base, i
             nx = or_quad((l << mag) | (r >> mag)) & ~(mine | theirs);
             if (nx == 0) player = 0;
         }
+        // the prior of a move (< 64) from the lane holding its transformed entry
+        const float prior = __shfl(pol_l, transform_action(sq, t));
         if (q == 0 && k < nc) {
             Pos c;
             c.player = player;
@@ -505,7 +508,7 @@ __device__ __forceinline__ void expand_quads(const EngineView& E, size_t base, i
             c.next_legal = nx;
             const int id = fc + k;
             store_link(E.link + base + id, NodeLink{-1, 0, leaf, c.player});
-            store_stat(E.stat + base + id, NodeStat{0, 0.0f, 0.0f, pol[transform_action(sq, t)]});
+            store_stat(E.stat + base + id, NodeStat{0, 0.0f, 0.0f, prior});
             store_pos(E.pos + base + id, c);
         }
     }
@@ -538,13 +541,18 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
         const int4 lk_v = *reinterpret_cast<const int4*>(E.link + base + leaf_v);
         const NodePos pos_v = E.pos[base + leaf_v];
         bool expanded_here = false;  // lane j: leaf j of this chunk expanded its node
-        // path of the chunk's first leaf; each leaf prefetches the next one's
+        // path and policy row (entry `lane`; the pass's entry 64 is read when used) of the chunk's first
+        // leaf; each leaf prefetches the next one's (the ResNet launch that
+        // wrote the rows has completed before this kernel started)
         int gp0 = 0, gp1 = 0;
+        float pol_l = 0.0f;
         {
             const int* gp = E.path + (size_t)(g * E.L + c0) * kMaxDepth;
             const int d0 = readlane_i(d_v, 0);
             if (lane >= 1 && lane <= d0) gp0 = gp[lane];
             if (64 + lane <= d0) gp1 = gp[64 + lane];
+            const float* pr = E.policy + (size_t)(g * E.L + c0) * 65;
+            pol_l = pr[lane];
         }
         for (int j = 0; j < cend; ++j) {
             const int r = g * E.L + c0 + j;
@@ -554,11 +562,14 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
             const NodeLink lk{readlane_i(lk_v.x, j), readlane_i(lk_v.y, j), readlane_i(lk_v.z, j),
                               readlane_i(lk_v.w, j)};
             const int path0 = gp0, path1 = gp1;
-            if (j + 1 < cend) {  // next leaf's path, behind this leaf's work
+            const float polj = pol_l;
+            if (j + 1 < cend) {  // next leaf's path and policy row, behind this leaf's work
                 const int* gp = E.path + (size_t)(r + 1) * kMaxDepth;
                 const int dn = readlane_i(d_v, j + 1);
                 if (lane >= 1 && lane <= dn) gp0 = gp[lane];
                 if (64 + lane <= dn) gp1 = gp[64 + lane];
+                const float* pr = E.policy + (size_t)(r + 1) * 65;
+                pol_l = pr[lane];
             }
             const bool already = __ballot(expanded_here && leaf_v == leaf) != 0;
             if (lk.player != 0 && lk.n_children == 0 && !already) {
@@ -575,13 +586,12 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
                 } else {
                     const int fc = count;
                     count += nc;
-                    const float* pol = E.policy + (size_t)r * 65;
                     if (P.legal) {
-                        expand_quads(E, base, leaf, P, fc, nc, t, pol);
+                        expand_quads(E, base, leaf, P, fc, nc, t, polj);
                     } else if (lane == 0) {  // the pass: one child (position.h:382-386)
                         const Pos c = apply_action(P, 64);
                         store_link(E.link + base + fc, NodeLink{-1, 0, leaf, c.player});
-                        store_stat(E.stat + base + fc, NodeStat{0, 0.0f, 0.0f, pol[64]});
+                        store_stat(E.stat + base + fc, NodeStat{0, 0.0f, 0.0f, E.policy[(size_t)r * 65 + 64]});
                         store_pos(E.pos + base + fc, c);
                     }
                     if (lane == 0) store_link(E.link + base + leaf, NodeLink{fc, nc, lk.parent, lk.player});

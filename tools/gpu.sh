@@ -17,6 +17,7 @@
 #                                  for bit with the first variant's
 #   stamps NAME VARIANT [VAR=val]  tools/nn_stamps.py with abv/VARIANT (built with -DOAMD_STAMPS)
 #   benchvar NAME [bench args]     bench line of every prebuilt variant, ROUNDS interleaved sweeps
+#   latvar NAME                    tools/latency.py with every prebuilt variant, ROUNDS sweeps
 #   treestamps NAME [VAR=val]      tools/tree_stamps.py with abv/ts (tools/tree_stamps_build.sh)
 #   records                        the canonical record set: tests, the C2 bench line (20 + 5 steps), kernel
 #                                  traces of C2 / 200 steps / C4 / C5, the C2 line under torch.distributed.run
@@ -94,6 +95,15 @@ run_recipe() {
           cp abv/$v/liboamd.so $PKG/liboamd.so
           step 600 "$OUT/benchvar_${n}_${v}_$r.json" env OAMD_AB_VARIANT=$v python bench.py --cpu-baseline-moves 0 \
             --deep-tree-moves 0 --latency-moves 0 --no-config-records "$@" || { restore_lib; return 1; }
+        done
+      done
+      restore_lib ;;
+    latvar) local n=$1; shift  # tools/latency.py with every prebuilt abv/<v>/liboamd.so
+      cp $PKG/liboamd.so /tmp/liboamd.so.orig
+      for r in $(seq ${ROUNDS:-2}); do
+        for v in ${AB_ORDER:-$(ls abv)}; do
+          cp abv/$v/liboamd.so $PKG/liboamd.so
+          step 300 "$OUT/latvar_${n}_${v}_$r.log" python tools/latency.py || { restore_lib; return 1; }
         done
       done
       restore_lib ;;

@@ -4,7 +4,8 @@
 #   VARIANTS="name:extra flags[:SRC];name2:..." bash tools/variants.sh
 # SRC: empty = the tree's resnet.hip with the tree's tree/capi objects; + =
 # every unit of the working tree built with the flags;
-# a path = that resnet.hip with the tree's tree/capi objects; @REV = all of
+# a path = that resnet.hip with the tree's tree/capi objects; tree=PATH = that
+# tree.hip with the working tree's other units; @REV = all of
 # csrc/ and include/ at git revision REV (capi.hip packs the weights, so a
 # variant that changes the packing must bring its own capi). Built into
 # abv/<name>/liboamd.so (the pybind layer binds the C ABI, not the variant).
@@ -27,6 +28,11 @@ for e in "${SETS[@]}"; do
     if [[ "${src:-}" == "+" ]]; then  # every unit of the working tree, built with the flags
       $CXX -I $CS -I include $flags $RF -c $CS/resnet.hip -o abv/$name/resnet.o
       $CXX -I $CS -I include $flags $EXACT $NOSCALAR -c $CS/tree.hip -o abv/$name/tree.o
+      $CXX -I $CS -I include $flags $EXACT -c $CS/capi.hip -o abv/$name/capi.o
+      objs="abv/$name/tree.o abv/$name/capi.o"
+    elif [[ "${src:-}" == tree=* ]]; then  # another tree.hip, the working tree's other units
+      $CXX -I $CS -I include $flags $RF -c $CS/resnet.hip -o abv/$name/resnet.o
+      $CXX -I $CS -I include $flags $EXACT $NOSCALAR -c ${src#tree=} -o abv/$name/tree.o
       $CXX -I $CS -I include $flags $EXACT -c $CS/capi.hip -o abv/$name/capi.o
       objs="abv/$name/tree.o abv/$name/capi.o"
     elif [[ "${src:-}" == @* ]]; then
