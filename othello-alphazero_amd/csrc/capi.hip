@@ -1668,88 +1668,96 @@ static int selfplay_steps_free(oamd_engine* e, oamd_net* net, const oamd_selfpla
     const int nch = e->nn_chains < K ? e->nn_chains : K;
     const int nlg = launches_per_group_round(e, P);
     if (int rc = fork_groups(e, P)) return rc;
-    for (int k = 0; k < K; ++k) {
-        HIPCHK(hipMemsetAsync(e->rowcount + 2 * k, 0, 2 * sizeof(int32_t), P.st[k]));
-        HIPCHK(hipMemsetAsync(e->remaining_dev + k, 0, sizeof(int32_t), P.st[k]));
-        launch_free_begin(E, P.g0[k], P.ng[k], n_moves, e->remaining_dev + k, actions, finished, per_move, P.st[k]);
-    }
-    bool gdone[kMaxPipeline] = {};
-    const int64_t base_rounds = n_moves > 0 ? (int64_t)n_moves * steps + 1 : 0;
-    // a round completes at least one batch of every game still playing (or
-    // its move): a generous bound that only a kernel fault could exceed
-    const int64_t max_rounds = base_rounds + (int64_t)n_moves * ((int64_t)T * steps + 2) + 4 * oamd_engine::kFreeTailRounds;
     int64_t round = 0;
-    for (int64_t chunk = 0; n_moves > 0; ++chunk) {
-        int R;
-        const bool tail = round >= base_rounds;
-        if (!tail) {
-            R = (int)std::min<int64_t>(round == 0 ? steps + 1 : steps, base_rounds - round);
-        } else {
-            if (chunk >= 2) {  // chunk - 2's readback: done by now while chunk - 1 is queued
-                const int slot = (int)((chunk - 2) % oamd_engine::kFreeSlots);
+    // everything between the fork and the join; on an error the groups are
+    // still joined into the caller's stream, so that nothing the caller
+    // enqueues next overlaps the rounds already in the group streams
+    auto rounds = [&]() -> int {
+        for (int k = 0; k < K; ++k) {
+            HIPCHK(hipMemsetAsync(e->rowcount + 2 * k, 0, 2 * sizeof(int32_t), P.st[k]));
+            HIPCHK(hipMemsetAsync(e->remaining_dev + k, 0, sizeof(int32_t), P.st[k]));
+            launch_free_begin(E, P.g0[k], P.ng[k], n_moves, e->remaining_dev + k, actions, finished, per_move, P.st[k]);
+        }
+        bool gdone[kMaxPipeline] = {};
+        const int64_t base_rounds = n_moves > 0 ? (int64_t)n_moves * steps + 1 : 0;
+        // a round completes at least one batch of every game still playing (or
+        // its move): a generous bound that only a kernel fault could exceed
+        const int64_t max_rounds = base_rounds + (int64_t)n_moves * ((int64_t)T * steps + 2) + 4 * oamd_engine::kFreeTailRounds;
+        for (int64_t chunk = 0; n_moves > 0; ++chunk) {
+            int R;
+            const bool tail = round >= base_rounds;
+            if (!tail) {
+                R = (int)std::min<int64_t>(round == 0 ? steps + 1 : steps, base_rounds - round);
+            } else {
+                if (chunk >= 2) {  // chunk - 2's readback: done by now while chunk - 1 is queued
+                    const int slot = (int)((chunk - 2) % oamd_engine::kFreeSlots);
+                    for (int k = 0; k < K; ++k) {
+                        if (gdone[k]) continue;
+                        HIPCHK(hipEventSynchronize(e->free_ev[slot][k]));
+                        if (e->remaining_host[slot * kMaxPipeline + k] == 0) gdone[k] = true;
+                    }
+                }
+                bool all = true;
+                for (int k = 0; k < K; ++k) all = all && gdone[k];
+                if (all) break;
+                if (round >= max_rounds) return fail(OAMD_RUNTIME, "free-running self-play did not finish");
+                R = oamd_engine::kFreeTailRounds;
+            }
+            bool timed = false;
+            if (!tail) {
+                if (int rc = timing_begin(e, R, K, &timed)) return rc;
+            }
+            const int pool = e->ev_cur;
+            unsigned long long* span = nullptr;
+            if (int rc = e->reserve_spans((int64_t)K * R * nlg, &span)) return rc;
+            for (int s = 0; s < R; ++s) {
+                const int64_t r = round + s;
                 for (int k = 0; k < K; ++k) {
                     if (gdone[k]) continue;
-                    HIPCHK(hipEventSynchronize(e->free_ev[slot][k]));
-                    if (e->remaining_host[slot * kMaxPipeline + k] == 0) gdone[k] = true;
+                    hipStream_t sk = P.st[k];
+                    hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
+                    int* cnt = e->rowcount + 2 * k;
+                    if (ev) HIPCHK(hipEventRecord(ev[0], sk));
+                    launch_tree_free(E, sk, P.g0[k], P.ng[k], B, cnt + (r & 1), cnt + ((r + 1) & 1), budget, timed, sp,
+                                     n_moves, per_move, actions, finished, feat, pol, e->remaining_dev + k);
+                    if (ev) HIPCHK(hipEventRecord(ev[1], sk));
+                    if (K > 1 && (r > 0 || k >= nch)) HIPCHK(hipStreamWaitEvent(sk, e->nn_token[k % nch], 0));
+                    if (ev) HIPCHK(hipEventRecord(ev[2], sk));
+                    const int grows = P.ng[k] * L;
+                    const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
+                    const size_t r0 = (size_t)P.g0[k] * L;
+                    for (int rr = 0, j = 0; rr < grows; rr += cb, ++j)
+                        launch_resnet_packed(N, E.feat, E.FW, E.H, std::min(cb, grows - rr), E.policy, E.value, sk,
+                                             E.rowlist + r0 + rr, cnt + (r & 1), rr,
+                                             span ? span + (size_t)2 * ((k * R + s) * nlg + j) : nullptr,
+                                             tail ? e->extra_grid : 0);
+                    if (ev) HIPCHK(hipEventRecord(ev[3], sk));
+                    if (K > 1) HIPCHK(hipEventRecord(e->nn_token[k % nch], sk));
                 }
             }
-            bool all = true;
-            for (int k = 0; k < K; ++k) all = all && gdone[k];
-            if (all) break;
-            if (round >= max_rounds) return fail(OAMD_RUNTIME, "free-running self-play did not finish");
-            R = oamd_engine::kFreeTailRounds;
-        }
-        bool timed = false;
-        if (!tail) {
-            if (int rc = timing_begin(e, R, K, &timed)) return rc;
-        }
-        const int pool = e->ev_cur;
-        unsigned long long* span = nullptr;
-        if (int rc = e->reserve_spans((int64_t)K * R * nlg, &span)) return rc;
-        for (int s = 0; s < R; ++s) {
-            const int64_t r = round + s;
+            const int slot = (int)(chunk % oamd_engine::kFreeSlots);
             for (int k = 0; k < K; ++k) {
                 if (gdone[k]) continue;
-                hipStream_t sk = P.st[k];
-                hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * K + k)] : nullptr;
-                int* cnt = e->rowcount + 2 * k;
-                if (ev) HIPCHK(hipEventRecord(ev[0], sk));
-                launch_tree_free(E, sk, P.g0[k], P.ng[k], B, cnt + (r & 1), cnt + ((r + 1) & 1), budget, timed, sp,
-                                 n_moves, per_move, actions, finished, feat, pol, e->remaining_dev + k);
-                if (ev) HIPCHK(hipEventRecord(ev[1], sk));
-                if (K > 1 && (r > 0 || k >= nch)) HIPCHK(hipStreamWaitEvent(sk, e->nn_token[k % nch], 0));
-                if (ev) HIPCHK(hipEventRecord(ev[2], sk));
-                const int grows = P.ng[k] * L;
-                const int cb = e->nn_batch > 0 ? e->nn_batch : grows;
-                const size_t r0 = (size_t)P.g0[k] * L;
-                for (int rr = 0, j = 0; rr < grows; rr += cb, ++j)
-                    launch_resnet_packed(N, E.feat, E.FW, E.H, std::min(cb, grows - rr), E.policy, E.value, sk,
-                                         E.rowlist + r0 + rr, cnt + (r & 1), rr,
-                                         span ? span + (size_t)2 * ((k * R + s) * nlg + j) : nullptr,
-                                         tail ? e->extra_grid : 0);
-                if (ev) HIPCHK(hipEventRecord(ev[3], sk));
-                if (K > 1) HIPCHK(hipEventRecord(e->nn_token[k % nch], sk));
+                HIPCHK(hipMemcpyAsync(e->remaining_host + slot * kMaxPipeline + k, e->remaining_dev + k, sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, P.st[k]));
+                HIPCHK(hipEventRecord(e->free_ev[slot][k], P.st[k]));
             }
+            if (timed) timing_end_rounds(e, R, P);
+            round += R;
         }
-        const int slot = (int)(chunk % oamd_engine::kFreeSlots);
-        for (int k = 0; k < K; ++k) {
-            if (gdone[k]) continue;
-            HIPCHK(hipMemcpyAsync(e->remaining_host + slot * kMaxPipeline + k, e->remaining_dev + k, sizeof(int32_t),
-                                  hipMemcpyDeviceToHost, P.st[k]));
-            HIPCHK(hipEventRecord(e->free_ev[slot][k], P.st[k]));
-        }
-        if (timed) timing_end_rounds(e, R, P);
-        round += R;
-    }
-    // the next search (or call) starts with empty evaluation lists
-    for (int k = 0; k < K; ++k) HIPCHK(hipMemsetAsync(e->rowcount + 2 * k, 0, 2 * sizeof(int32_t), P.st[k]));
-    e->grouped_searches += n_moves;
-    e->grouped_rounds += round;
-    LAUNCHCHK();
-    if (int rc = join_groups(e, P)) return rc;
+        // the next search (or call) starts with empty evaluation lists
+        for (int k = 0; k < K; ++k) HIPCHK(hipMemsetAsync(e->rowcount + 2 * k, 0, 2 * sizeof(int32_t), P.st[k]));
+        LAUNCHCHK();
+        return OAMD_OK;
+    };
+    const int rc = rounds();
+    const int jrc = join_groups(e, P);
     e->step_phase = 0;
     e->steps_left = 0;
-    return OAMD_OK;
+    if (rc) return rc;
+    e->grouped_searches += n_moves;
+    e->grouped_rounds += round;
+    return jrc;
 }
 
 int oamd_engine_set_free_running(oamd_engine* e, int32_t enable) {
