@@ -12,6 +12,7 @@
 #   nn NAME [VAR=val ...]          standalone k_resnet timing (tools/nn_kernel.py; ROWS, NN_C, NN_DTYPE)
 #   nnpmc NAME C1,C2,.. [VAR=val]  one --pmc pass over tools/nn_kernel.py  -> nnpmc_NAME/
 #   latency NAME                   single-game latency (tools/latency.py)
+#   stress NAME [MOVES CHUNK]      free-running vs lock step over many game generations (tools/stress_free.py)
 #   variants NAME [VAR=val ...]    nn timing of every prebuilt abv/<v>/liboamd.so (tools/variants.sh
 #                                  builds them here), ROUNDS interleaved sweeps, outputs compared bit
 #                                  for bit with the first variant's
@@ -68,6 +69,7 @@ run_recipe() {
       step 300 "$OUT/nnpmc_$n.log" env "$@" rocprofv3 --pmc ${c//,/ } --kernel-trace -d "$OUT/nnpmc_$n" \
         -o run --output-format csv -- python3 tools/nn_kernel.py ;;
     latency) step 600 "$OUT/latency_$1.log" python tools/latency.py ;;
+    stress) step 900 "$OUT/stress_$1.log" python -u tools/stress_free.py "${@:2}" ;;
     variants) local n=$1; shift
       cp $PKG/liboamd.so /tmp/liboamd.so.orig
       local ref=/tmp/ab_ref_$n.pt; rm -f $ref
