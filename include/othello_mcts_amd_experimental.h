@@ -59,9 +59,10 @@ int oamd_engine_set_adaptive_extra_rounds(oamd_engine *e, int32_t enable, int32_
  * over them instead of dispatching ~1000 mostly empty workgroups between the
  * other NN chain's. Scheduling only: results are identical. */
 int oamd_engine_set_extra_round_grid(oamd_engine *e, int32_t workgroups);
-/* Diagnostics: copy the ResNet kernel's per-workgroup time stamps (8 u64 per
- * workgroup, 16 u64 per workgroup: see tools/nn_stamps.py) of the last launch. Only in builds
- * with OAMD_EXTRA_FLAGS=-DOAMD_STAMPS; otherwise OAMD_INVALID_ARGUMENT. */
+/* Diagnostics: copy the ResNet kernel's per-workgroup time stamps and cycle
+ * sums (24 u64 per workgroup, resnet.hip kStampStride; see tools/nn_stamps.py)
+ * of the last launch. Only in builds with OAMD_EXTRA_FLAGS=-DOAMD_STAMPS;
+ * otherwise OAMD_INVALID_ARGUMENT. */
 int oamd_debug_read_stamps(uint64_t *out, int64_t n);
 /* Diagnostics: k_tree's phase cycle sums over every wave since the last reset
  * (tools/tree_stamps.py); reset != 0 zeroes them after the copy. Only in
