@@ -214,19 +214,24 @@ __device__ __forceinline__ int child_index_of(uint64_t legal, int n_children, in
     return popcount64(legal & (~0ULL << (64 - action)));
 }
 
-// Fill the packed features of row r: leaf = path[d]; ancestors continue into
-// the game history (position_iterator.h:24-71, transformation.h:83-116).
-__device__ __forceinline__ void write_packed_features(const EngineView& E, size_t base, int r,
-                                                      int d, int p0, int p1, int hist_node,
-                                                      int hist_n, int leaf_player, int t,
-                                                      bool valid) {
-    const int lane = lane_id();
+// Packed features of row r (position_iterator.h:24-71, transformation.h:83-116):
+// a meta word (leaf player, symmetry, valid; 0 for a terminal leaf: no NN row)
+// and the H positions leaf = path[d], its ancestors, then the game history.
+// The meta word is written at the leaf; the positions are gathered for up to
+// 64 / H leaves at once (flush_ancestors), so the selection loop does not wait
+// for a position load per leaf.
+__device__ __forceinline__ void write_feature_meta(const EngineView& E, int r, int leaf_player, int t,
+                                                   bool valid) {
+    if (lane_id() != 0) return;
     uint64_t* row = E.feat + (size_t)r * E.FW;
-    if (!valid) {  // a terminal leaf: no NN row, only the meta word says so
-        if (lane == 0) row[0] = 0ULL;
-        return;
-    }
-    // ancestor h = path[d - h] for h <= d, else hist[h - d - 1]
+    row[0] = valid ? ((uint64_t)((leaf_player - 1) & 1) | ((uint64_t)t << 8) | (1ULL << 16)) : 0ULL;
+    row[1] = 0;
+}
+
+// Node of position h = lane (< H) of a leaf at depth d: path[d - h] for h <= d,
+// else hist[h - d - 1]; -1 past the history (a zero plane pair)
+__device__ __forceinline__ int feature_ancestor(int d, int p0, int p1, int hist_node, int hist_n) {
+    const int lane = lane_id();
     const int idx = d - lane;
     const int from_p0 = __shfl(p0, idx & 63);
     const int from_p1 = __shfl(p1, idx & 63);
@@ -235,21 +240,26 @@ __device__ __forceinline__ void write_packed_features(const EngineView& E, size_
     int anc = -1;
     if (idx >= 0) anc = idx < 64 ? from_p0 : from_p1;
     else if (hj < hist_n) anc = from_h;
+    return anc;
+}
+
+// Position planes of rows r0 .. r0 + n - 1: lane j = (leaf j / H, position
+// j % H) holds its node in anc (from feature_ancestor); bit k of `valid` =
+// row r0 + k has an NN row. One load round trip for all of them.
+__device__ __forceinline__ void flush_ancestors(const EngineView& E, size_t base, int r0, int n, int anc,
+                                                uint64_t valid) {
+    const int lane = lane_id();
+    const int k = lane / E.H, h = lane - k * E.H;
+    if (k >= n || !((valid >> k) & 1ULL)) return;
     uint64_t a1 = 0, a2 = 0;
-    if (lane < E.H && anc >= 0) {
+    if (anc >= 0) {
         const NodePos* np = E.pos + base + anc;
         a1 = np->p1;
         a2 = np->p2;
     }
-    if (lane < E.H) {
-        row[2 + 2 * lane] = a1;
-        row[3 + 2 * lane] = a2;
-    }
-    if (lane == 0) {
-        const uint64_t meta = (uint64_t)((leaf_player - 1) & 1) | ((uint64_t)t << 8) | (1ULL << 16);
-        row[0] = meta;
-        row[1] = 0;
-    }
+    uint64_t* row = E.feat + (size_t)(r0 + k) * E.FW;
+    row[2 + 2 * h] = a1;
+    row[3 + 2 * h] = a2;
 }
 
 // Append the NN rows of non-terminal leaves among rows c0 + j (bit j of
@@ -288,6 +298,10 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
     int root_n = E.stat[base + root].n;
     uint64_t valid_rows = 0;  // bit i - c0: row i is an NN row (chunks of 64 rows from i0)
     int c0 = i0;
+    // feature positions of leaves f0 .. (up to 64 / H of them), flushed together
+    const int per_flush = 64 / E.H;
+    int f0 = i0, anc_rec = -1;
+    uint64_t fvalid = 0;
 
     for (int i = i0; i < i1; ++i) {
         const int r = g * E.L + i;
@@ -387,7 +401,19 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
             E.depth[r] = d;
             E.trans[r] = t;
         }
-        write_packed_features(E, base, r, d, p0, p1, hist_node, hist_n, lk.player, t, valid);
+        write_feature_meta(E, r, lk.player, t, valid);
+        {
+            const int anc = feature_ancestor(d, p0, p1, hist_node, hist_n);
+            const int k = i - f0;
+            const int moved = __shfl(anc, (lane - k * E.H) & 63);
+            if (lane >= k * E.H && lane < (k + 1) * E.H) anc_rec = moved;
+            fvalid |= (uint64_t)(valid ? 1 : 0) << k;
+            if (k == per_flush - 1 || i == i1 - 1) {
+                flush_ancestors(E, base, g * E.L + f0, k + 1, anc_rec, fvalid);
+                f0 = i + 1;
+                fvalid = 0;
+            }
+        }
         sims += 1;
         evals += valid ? 1 : 0;
         depth_sum += (unsigned long long)d;
@@ -803,7 +829,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
                     E.depth[r] = 0;
                     E.trans[r] = 0;
                 }
-                write_packed_features(E, base, r, 0, 0, 0, -1, 0, 1, 0, false);
+                write_feature_meta(E, r, 1, 0, false);
             }
         }
         return;
