@@ -298,6 +298,15 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
     int root_n = E.stat[base + root].n;
     uint64_t valid_rows = 0;  // bit i - c0: row i is an NN row (chunks of 64 rows from i0)
     int c0 = i0;
+    // Root noise vectors drawn ahead: lane s * nz_nc + j holds the noise of
+    // child j at event nz_base + s, for as many events as 64 lanes hold (a
+    // selection followed by a non-terminal leaf's symmetry draw uses two, one
+    // ending in a terminal leaf one); a selection past them draws again.
+    // The noise is a function of (game key, event, child) only, so these are
+    // the draws of the selections themselves.
+    float nz_cache = 0.0f;
+    uint64_t nz_base = ~0ULL;
+    int nz_nc = 0;
     // feature positions of leaves f0 .. (up to 64 / H of them), flushed together
     const int per_flush = 64 / E.H;
     int f0 = i0, anc_rec = -1;
@@ -335,8 +344,17 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
                 float prob = cs.p;
                 if (node == root && E.eps > 0.0f) {
                     // fresh Dirichlet noise on every root selection (search_thread.cpp:230-249)
-                    float noise = 0.0f;
-                    if (lane < nc) noise = gamma_draw(stream_key(key, event, (uint32_t)lane), E.alpha);
+                    const int slots = 64 / nc;
+                    const uint64_t off = event - nz_base;
+                    if (nz_nc != nc || off >= (uint64_t)slots) {
+                        nz_base = event;
+                        nz_nc = nc;
+                        const int sl = lane / nc, j = lane - sl * nc;
+                        nz_cache = sl < slots ? gamma_draw(stream_key(key, event + (uint64_t)sl, (uint32_t)j), E.alpha)
+                                              : 0.0f;
+                    }
+                    float noise = __shfl(nz_cache, ((int)(event - nz_base) * nc + lane) & 63);
+                    if (lane >= nc) noise = 0.0f;
                     event += 1;
                     float nsum = 0.0f;
                     for (int j = 0; j < nc; ++j) nsum += readlane_f(noise, j);
