@@ -816,9 +816,9 @@ __device__ __forceinline__ void add_counters(const EngineView& E, const RoundAcc
     }
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree(EngineView E, int g0, int do_backup, int do_select,
-                                             int t0, int t1, int B, int* cnt_add, int* cnt_reset, int fresh,
-                                             int budget, int max_cuts, int timed, int* cuts_out) {
+__device__ __forceinline__ void tree_round_kernel(const EngineView& E, int g0, int do_backup, int do_select, int t0,
+                                                  int t1, int B, int* cnt_add, int* cnt_reset, int fresh, int budget,
+                                                  int max_cuts, int timed, int* cuts_out) {
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
@@ -893,6 +893,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
 #endif
         if (do_select) add_counters(E, acc, timed != 0);
     }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tree(EngineView E, int g0, int do_backup,
+                                                                                int do_select, int t0, int t1, int B,
+                                                                                int* cnt_add, int* cnt_reset, int fresh,
+                                                                                int budget, int max_cuts, int timed,
+                                                                                int* cuts_out) {
+    tree_round_kernel(E, g0, do_backup, do_select, t0, t1, B, cnt_add, cnt_reset, fresh, budget, max_cuts, timed,
+                      cuts_out);
+}
+
+// The same round without the register cap (114 VGPRs, no spills) for launches
+// of at most kWideTreeGames games (the single-game drop-in MCTS and other
+// small engines): their NN launches leave most CUs free, so a tree wave needs
+// no room beside ResNet waves, and its leaves' serial chain is the search's
+// critical path.
+constexpr int kWideTreeGames = 16;
+__global__ __launch_bounds__(64) void k_tree_wide(EngineView E, int g0, int do_backup, int do_select, int t0, int t1,
+                                                  int B, int* cnt_add, int* cnt_reset, int fresh, int budget,
+                                                  int max_cuts, int timed, int* cuts_out) {
+    tree_round_kernel(E, g0, do_backup, do_select, t0, t1, B, cnt_add, cnt_reset, fresh, budget, max_cuts, timed,
+                      cuts_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -1405,9 +1427,9 @@ void launch_tree(const EngineView& E, hipStream_t s, bool do_backup, bool do_sel
     if (t1 < 0) t1 = T;
     if (T * B != E.L || t0 < 0 || t1 > T || t0 >= t1) return;  // caller validated; never launch on a mismatched layout
     if (ng > 0 && (do_backup || do_select))
-        hipLaunchKernelGGL(k_tree, dim3(ng), dim3(64), 0, s, E, g0, (int)do_backup, (int)do_select, t0, t1, B,
-                           do_select ? cnt_add : nullptr, cnt_reset, (int)fresh, budget, max_cuts, (int)timed,
-                           cuts_out);
+        hipLaunchKernelGGL(ng <= kWideTreeGames ? k_tree_wide : k_tree, dim3(ng), dim3(64), 0, s, E, g0,
+                           (int)do_backup, (int)do_select, t0, t1, B, do_select ? cnt_add : nullptr, cnt_reset,
+                           (int)fresh, budget, max_cuts, (int)timed, cuts_out);
 }
 void launch_features_f32(const EngineView& E, float* out, int row_begin, int rows, hipStream_t s) {
     if (rows > 0) hipLaunchKernelGGL(k_features_f32, dim3(blocks_for(rows, 4)), dim3(256), 0, s, E, out, row_begin, rows);

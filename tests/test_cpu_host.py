@@ -367,6 +367,7 @@ def test_k_tree_reads_no_written_state_through_the_scalar_cache(tmp_path):
     wave's vector stores. build.py compiles tree.hip with
     -amdgpu-scalarize-global-loads=false, so no global load is scalarised;
     the gfx950 ISA of the built kernels confirms it: every s_load of k_tree
+    (and of its uncapped twin k_tree_wide)
     reads the kernel arguments (one base register, offsets inside the
     argument segment), and every s_load of k_tree_free (which reloads its
     arguments into other registers) lies inside its argument segment."""
@@ -404,7 +405,7 @@ def test_k_tree_reads_no_written_state_through_the_scalar_cache(tmp_path):
             bodies[cur] = []
         elif cur:
             bodies[cur].append(ln.strip())
-    for key, single_base in (("6k_tree", True), ("11k_tree_free", False)):
+    for key, single_base in (("6k_tree", True), ("11k_tree_wide", True), ("11k_tree_free", False)):
         sym = next(n for n in bodies if n.startswith(f"_ZN4oamd{key}E"))
         body = bodies[sym]
         assert len(body) > 1000, sym
