@@ -36,7 +36,7 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #ifdef OAMD_TREE_STAMPS
 enum TreeStamp {
     kTsWaves, kTsCycles, kTsDescent, kTsLevels, kTsLeaves, kTsPost, kTsBackup, kTsBackedUp, kTsTerminal,
-    kTsMaxCycles, kTsBatches, kTsSelect, kTsCount
+    kTsMaxCycles, kTsBatches, kTsSelect, kTsExpand, kTsPathW, kTsCount
 };
 __device__ unsigned long long g_tree_stamps[kTsCount];
 __shared__ unsigned long long ts_acc[kTsCount];
@@ -616,6 +616,7 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
                 pol_l = pr[lane];
             }
             const bool already = __ballot(expanded_here && leaf_v == leaf) != 0;
+            TS_T(te0);
             if (lk.player != 0 && lk.n_children == 0 && !already) {
                 Pos P;
                 P.player = lk.player;
@@ -642,6 +643,8 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
                     if (lane == j) expanded_here = true;
                 }
             }
+            TS_T(te1);
+            TS_ADD(kTsExpand, te1 - te0);
             if (d > 0) {
                 float v;
                 if (lk.player != 0) {
@@ -674,6 +677,8 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
                 }
             }
             wave_order();  // the next leaf's backup reads these statistics
+            TS_T(tw1);
+            TS_ADD(kTsPathW, tw1 - te1);
         }
     }
     TS_T(tb1);

@@ -292,6 +292,38 @@ def test_selfplay_steps_equal_move_by_move(om, G, pipeline):
                     f"{n} moves identical to search + selfplay_move, {restarts} game ends")
 
 
+def test_wide_and_capped_tree_kernels_agree(om):
+    """k_tree_wide (launches of <= 16 games, no register cap) and k_tree (the
+    96-VGPR cap) run the same rounds: 32 games as one pipeline group (k_tree)
+    and as 2 or 4 groups (k_tree_wide), with root noise (the drawn-ahead noise
+    windows) and endings inside the moves: actions, finish codes and trees
+    equal bit for bit."""
+    from othello_mcts.synthetic import alphazero_state_dict
+
+    net = om.NativeNet(alphazero_state_dict(37, 9, 128, 2, 64), device=0)
+    outs = {}
+    for pipeline in (1, 2, 4):
+        b = om.BatchedMCTS(32, history_size=4, num_simulations=160, num_threads=2, batch_size=8, seed=19,
+                           dirichlet_epsilon=0.25, node_capacity=1 << 15)
+        b.random_openings(53, seed=23)  # 7 empties: games end within the 8 moves
+        b.engine.set_pipeline(pipeline)
+        acts, fins = [], []
+        for _ in range(8):
+            b.search(net, sync=False)
+            o = b.selfplay_move(temperature_moves=12, opening_moves=4)
+            acts.append(o["actions"].clone())
+            fins.append(o["finished"].clone())
+        torch.cuda.synchronize()
+        assert b.engine.status() == (0, 0)
+        outs[pipeline] = (torch.stack(acts), torch.stack(fins), *b.root_stats())
+    for pipeline in (2, 4):
+        for x, y in zip(outs[1], outs[pipeline]):
+            assert torch.equal(x, y), pipeline
+    ends = int(((outs[1][1] & 3) != 0).sum())
+    assert ends > 0
+    numerics.record("k_tree_wide == k_tree", f"32 games x 8 moves, eps 0.25, {ends} game ends, groups of 32 / 16 / 8")
+
+
 @pytest.mark.parametrize("T,B,nn_batch,pipeline,exact", [(3, 8, 0, 0, True), (4, 4, 384, 3, True),
                                                          (2, 16, 0, 0, False)])
 def test_free_running_schedules_equal_lock_step(om, T, B, nn_batch, pipeline, exact):
