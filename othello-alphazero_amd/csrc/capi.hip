@@ -1392,15 +1392,20 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     const int K = P.K;
     const int T = e->cfg.num_threads, B = e->cfg.batch_size;
     // One game with T > 1 virtual threads (the drop-in MCTS, latency mode):
-    // the tree kernel runs thread by thread on the engine stream, and thread
-    // t's ResNet rows go to a stream of their own as soon as its selection is
-    // done, so they are evaluated while the tree kernel backs up and selects
+    // virtual thread t's tree operations (backup of its batch s-1 + selection
+    // of batch s) and its ResNet launches alternate on a stream of its own, so
+    // thread t's rows are evaluated while the tree kernel backs up and selects
     // for thread t+1 (the overlap the reference gets from its T threads,
-    // search_thread.cpp:59-128). The order of the tree operations is the same
-    // as in one launch per round, so results are identical.
+    // search_thread.cpp:59-128). The tree operations keep the order of one
+    // launch per round (thread 0 .. T-1, round by round) through an event
+    // from each to the next, so results are identical; an operation waits
+    // across streams only for the previous thread's tree operation, which ends
+    // while this thread's ResNet launch still runs (a ResNet launch waiting
+    // across streams for its selection, and a selection for its thread's
+    // launch, each cost ~13 us of queue latency per round).
     const bool split = e->G == 1 && K == 1 && T > 1 && T <= kMaxPipeline && e->tree_split();
     const int NB = split ? T : K;  // timing blocks per round
-    int rc = split ? e->ensure_streams(2, T) : e->ensure_streams(K, K);
+    int rc = split ? e->ensure_streams(T, T) : e->ensure_streams(K, K);
     if (rc) return rc;
     if (!split) P = plan_groups(e);  // the group streams exist now
     if (sims || evals) HIPCHK(hipMemsetAsync(e->counters, 0, 2 * sizeof(unsigned long long), e->stream));
@@ -1414,23 +1419,32 @@ int oamd_engine_search(oamd_engine* e, oamd_net* net, int64_t* sims, int64_t* ev
     const int pool = e->ev_cur;
     unsigned long long* span = nullptr;  // busy-time slots [thread][round] of the split schedule
     if (split && (rc = e->reserve_spans((int64_t)T * steps, &span))) return rc;
+    if (split) {  // every thread stream after the caller's stream
+        HIPCHK(hipEventRecord(e->fork_ev, e->stream));
+        for (int t = 0; t < T; ++t) HIPCHK(hipStreamWaitEvent(e->pipe_stream[t], e->fork_ev, 0));
+    }
     for (int s = 0; split && s <= steps; ++s) {
         for (int t = 0; t < T; ++t) {
             hipEvent_t* ev = timed ? &e->ev[pool][kEvPerBlock * (s * T + t)] : nullptr;
-            if (s > 0) HIPCHK(hipStreamWaitEvent(e->stream, e->nn_ev[t], 0));  // thread t's batch s-1 evaluated
-            if (ev) HIPCHK(hipEventRecord(ev[0], e->stream));
-            launch_tree(E, e->stream, s > 0, s < steps, T, B, 0, 1, t, t + 1, nullptr, nullptr, s == 0, 0, 0, timed);
-            if (ev) HIPCHK(hipEventRecord(ev[1], e->stream));
+            hipStream_t ts = e->pipe_stream[t];  // after this thread's batch s-1 evaluation (stream order)
+            if (s > 0 || t > 0)  // after the previous tree operation (thread t-1, or T-1 of round s-1)
+                HIPCHK(hipStreamWaitEvent(ts, e->sel_ev[t > 0 ? t - 1 : T - 1], 0));
+            if (ev) HIPCHK(hipEventRecord(ev[0], ts));
+            launch_tree(E, ts, s > 0, s < steps, T, B, 0, 1, t, t + 1, nullptr, nullptr, s == 0, 0, 0, timed);
+            if (ev) HIPCHK(hipEventRecord(ev[1], ts));
+            HIPCHK(hipEventRecord(e->sel_ev[t], ts));
             if (s == steps) continue;
-            hipStream_t ns = e->pipe_stream[t % 2];
-            HIPCHK(hipEventRecord(e->sel_ev[t], e->stream));
-            HIPCHK(hipStreamWaitEvent(ns, e->sel_ev[t], 0));
-            if (ev) HIPCHK(hipEventRecord(ev[2], ns));
+            if (ev) HIPCHK(hipEventRecord(ev[2], ts));
             launch_resnet_packed(N, E.feat + (size_t)t * B * E.FW, E.FW, E.H, B, E.policy + (size_t)t * B * 65,
-                                 E.value + (size_t)t * B, ns, nullptr, nullptr, 0,
+                                 E.value + (size_t)t * B, ts, nullptr, nullptr, 0,
                                  span ? span + (size_t)2 * (t * steps + s) : nullptr);
-            if (ev) HIPCHK(hipEventRecord(ev[3], ns));
-            HIPCHK(hipEventRecord(e->nn_ev[t], ns));
+            if (ev) HIPCHK(hipEventRecord(ev[3], ts));
+        }
+    }
+    if (split) {  // the caller's stream after every thread stream
+        for (int t = 0; t < T; ++t) {
+            HIPCHK(hipEventRecord(e->join_ev[t], e->pipe_stream[t]));
+            HIPCHK(hipStreamWaitEvent(e->stream, e->join_ev[t], 0));
         }
     }
     if (!split) {

@@ -12,6 +12,7 @@
 #   nn NAME [VAR=val ...]          standalone k_resnet timing (tools/nn_kernel.py; ROWS, NN_C, NN_DTYPE)
 #   nnpmc NAME C1,C2,.. [VAR=val]  one --pmc pass over tools/nn_kernel.py  -> nnpmc_NAME/
 #   latency NAME                   single-game latency (tools/latency.py)
+#   lattrace NAME SIMS             kernel trace of single-game searches (tools/latency_trace.py; EPS env)
 #   stress NAME [MOVES CHUNK]      free-running vs lock step over many game generations (tools/stress_free.py)
 #   variants NAME [VAR=val ...]    nn timing of every prebuilt abv/<v>/liboamd.so (tools/variants.sh
 #                                  builds them here), ROUNDS interleaved sweeps, outputs compared bit
@@ -61,6 +62,9 @@ run_recipe() {
     trace) local n=$1; shift
       step 600 "$OUT/trace_$n.log" rocprofv3 --kernel-trace --stats -T -d "$OUT/trace_$n" -o run \
         --output-format csv -- python3 bench.py "$@" ;;
+    lattrace) local n=$1 sims=$2  # kernel trace of single-game searches (EPS from the environment)
+      step 600 "$OUT/lattrace_$n.log" rocprofv3 --kernel-trace -T -d "$OUT/lattrace_$n" -o run \
+        --output-format csv -- python3 tools/latency_trace.py "$sims" ;;
     pmc) local n=$1 c=$2; shift 2
       step 300 "$OUT/pmc_$n.log" rocprofv3 --pmc ${c//,/ } --kernel-trace -T -d "$OUT/pmc_$n" -o run \
         --output-format csv -- python3 bench.py "$@" ;;
