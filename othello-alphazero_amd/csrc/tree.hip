@@ -705,7 +705,8 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
 // units of 2 on gfx950) so that a tree wave fits beside the two 208-VGPR
 // k_resnet_w8 waves of every SIMD (512 VGPRs): one pipeline group's tree round
 // runs on the CUs that the other group's ResNet launch occupies. The cap costs
-// two 8-byte spills outside the descent/backup loops.
+// 56 bytes per lane of spills (60 in k_tree_free); launches of at most
+// kWideTreeGames games run k_tree_wide, the same round uncapped (114 VGPRs).
 // Evaluation list (cnt_add != nullptr, the native search): the rows of
 // non-terminal leaves this round selects are appended to E.rowlist[g0 * L ..]
 // behind the counter *cnt_add; *cnt_reset (the counter of the next round,
