@@ -239,11 +239,32 @@ float orc_expf(float x) {
     return p * as_float((uint32_t)(k + 127) << 23);
 }
 
-/* Marsaglia–Tsang Gamma(alpha,1); alpha<1 via the U^(1/alpha) boost; normal
- * deviates by the Marsaglia polar method. Every loop is bounded so the GPU
- * wave always terminates; the bounded fallbacks are part of the spec. */
+/* cos^2(2 pi v), v in (0,1), folded to [0, pi/4] (rng.h cos2pi_sq) */
+float orc_cos2pi_sq(float v) {
+    float t = 2.0f * v;
+    t = t - floorf(t);
+    if (t > 0.5f) t = 1.0f - t;
+    float c;
+    if (t < 0.25f) {
+        float x = 3.14159274f * t;
+        float x2 = x * x;
+        c = 1.0f + x2 * (-0.5f + x2 * (0.0416666679f + x2 * (-0.00138888892f + x2 * 2.48015876e-05f)));
+    } else {
+        float x = 3.14159274f * (0.5f - t);
+        float x2 = x * x;
+        c = x * (1.0f + x2 * (-0.166666672f + x2 * (0.00833333377f + x2 * -0.000198412701f)));
+    }
+    return c * c;
+}
+
+/* Gamma(alpha,1). alpha = 1/2: Z^2/2 in Box-Muller form, -ln(U) cos^2(2 pi V)
+ * (no rejection). Otherwise Marsaglia–Tsang; alpha<1 via the U^(1/alpha)
+ * boost; normal deviates by the Marsaglia polar method. Every loop is bounded
+ * so the GPU wave always terminates; the bounded fallbacks are part of the
+ * spec. (rng.h gamma_draw) */
 float orc_gamma(uint64_t key, float alpha) {
     if (!(alpha > 0.0f)) return 0.0f;
+    if (alpha == 0.5f) return -orc_logf(orc_uniform(key, 0)) * orc_cos2pi_sq(orc_uniform(key, 1));
     uint32_t k = 0;
     int boost = alpha < 1.0f;
     float a = boost ? alpha + 1.0f : alpha;

@@ -67,6 +67,7 @@ float orc_logf(float x);
 float orc_expf(float x);
 /* Gamma(alpha, 1) draw consuming uniforms of one stream */
 float orc_gamma(uint64_t stream_key, float alpha);
+float orc_cos2pi_sq(float v);
 
 /* ---- MCTS (search_thread.cpp / mcts.cpp) ------------------------------ */
 typedef void (*orc_nn_fn)(void *user, const float *features, int rows, int channels,

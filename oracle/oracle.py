@@ -77,6 +77,7 @@ def lib():
             "orc_logf": (f32, [f32]),
             "orc_expf": (f32, [f32]),
             "orc_gamma": (f32, [u64, f32]),
+            "orc_cos2pi_sq": (f32, [f32]),
             "orc_mcts_create": (vp, [i32, i32, i32, i32, f32, f32, f32, f32, u64]),
             "orc_mcts_destroy": (None, [vp]),
             "orc_mcts_reset_position": (None, [vp]),

@@ -86,9 +86,32 @@ OAMD_HD float pexpf(float x) {
     return p * bits_to_float((uint32_t)(k + 127) << 23);
 }
 
-// Marsaglia–Tsang Gamma(alpha, 1) with the alpha < 1 boost; bounded loops.
+// cos^2(2 pi v) for v in (0, 1): folded to an argument x in [0, pi/4] of a
+// sine or cosine polynomial (plain float operations, as plogf)
+OAMD_HD float cos2pi_sq(float v) {
+    float t = 2.0f * v;
+    t = t - floorf(t);              // cos^2(pi t), period 1
+    if (t > 0.5f) t = 1.0f - t;     // symmetric about 1/2: t in [0, 1/2]
+    float c;
+    if (t < 0.25f) {                // cos(pi t), pi t in [0, pi/4)
+        const float x = 3.14159274f * t;
+        const float x2 = x * x;
+        c = 1.0f + x2 * (-0.5f + x2 * (0.0416666679f + x2 * (-0.00138888892f + x2 * 2.48015876e-05f)));
+    } else {                        // sin(pi (1/2 - t)), pi (1/2 - t) in [0, pi/4]
+        const float x = 3.14159274f * (0.5f - t);
+        const float x2 = x * x;
+        c = x * (1.0f + x2 * (-0.166666672f + x2 * (0.00833333377f + x2 * -0.000198412701f)));
+    }
+    return c * c;
+}
+
+// Gamma(alpha, 1). alpha = 1/2 (the default Dirichlet alpha): Z^2 / 2 for a
+// standard normal Z in Box-Muller form, -ln(U) cos^2(2 pi V), with no
+// rejection loop (a wave's lanes all finish together). Otherwise
+// Marsaglia–Tsang with the alpha < 1 boost; bounded loops.
 OAMD_HD float gamma_draw(uint64_t key, float alpha) {
     if (!(alpha > 0.0f)) return 0.0f;
+    if (alpha == 0.5f) return -plogf(uniform(key, 0)) * cos2pi_sq(uniform(key, 1));
     uint32_t k = 0;
     const bool boost = alpha < 1.0f;
     const float a = boost ? alpha + 1.0f : alpha;

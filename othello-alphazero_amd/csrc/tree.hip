@@ -36,7 +36,7 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #ifdef OAMD_TREE_STAMPS
 enum TreeStamp {
     kTsWaves, kTsCycles, kTsDescent, kTsLevels, kTsLeaves, kTsPost, kTsBackup, kTsBackedUp, kTsTerminal,
-    kTsMaxCycles, kTsBatches, kTsSelect, kTsExpand, kTsPathW, kTsCount
+    kTsMaxCycles, kTsBatches, kTsSelect, kTsExpand, kTsPathW, kTsNoise, kTsRefill, kTsCount
 };
 __device__ unsigned long long g_tree_stamps[kTsCount];
 __shared__ unsigned long long ts_acc[kTsCount];
@@ -344,14 +344,18 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
                 float prob = cs.p;
                 if (node == root && E.eps > 0.0f) {
                     // fresh Dirichlet noise on every root selection (search_thread.cpp:230-249)
+                    TS_T(tn0);
                     const int slots = 64 / nc;
                     const uint64_t off = event - nz_base;
                     if (nz_nc != nc || off >= (uint64_t)slots) {
+                        TS_T(tr0);
                         nz_base = event;
                         nz_nc = nc;
                         const int sl = lane / nc, j = lane - sl * nc;
                         nz_cache = sl < slots ? gamma_draw(stream_key(key, event + (uint64_t)sl, (uint32_t)j), E.alpha)
                                               : 0.0f;
+                        TS_T(tr1);
+                        TS_ADD(kTsRefill, tr1 - tr0);
                     }
                     float noise = __shfl(nz_cache, ((int)(event - nz_base) * nc + lane) & 63);
                     if (lane >= nc) noise = 0.0f;
@@ -362,6 +366,8 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
                     const float pm = 1.0f - E.eps;
                     const float nm = E.eps / nsum;
                     prob = cs.p * pm + noise * nm;
+                    TS_T(tn1);
+                    TS_ADD(kTsNoise, tn1 - tn0);
                 }
                 float ucb = cs.q + mult * prob / (1.0f + (float)cs.n);
                 if (lane >= nc) ucb = -__builtin_inff();

@@ -158,6 +158,20 @@ def test_random_streams_distributions():
     assert stats.chisquare(counts).pvalue > 1e-3
 
 
+def test_gamma_half_box_muller_form():
+    """alpha = 1/2 (the default): Gamma(1/2) = Z^2/2 = -ln(U) cos^2(2 pi V)
+    (rng.h gamma_draw): the folded cos^2 polynomial against libm over (0, 1),
+    and the draw is exactly that product of the stream's first two uniforms."""
+    L = O.lib()
+    vs = (2.0 * np.arange(0, 1 << 23, 997) + 1.0) / float(1 << 24)
+    c2 = np.array([L.orc_cos2pi_sq(float(v)) for v in vs])
+    assert np.max(np.abs(c2 - np.cos(2 * np.pi * vs) ** 2)) < 1e-6
+    for e in range(200):
+        k = L.orc_stream_key(3, e, 1)
+        want = np.float32(-L.orc_logf(L.orc_uniform(k, 0))) * np.float32(L.orc_cos2pi_sq(L.orc_uniform(k, 1)))
+        assert np.float32(L.orc_gamma(k, 0.5)) == want
+
+
 def test_portable_math_close_to_libm():
     xs = np.linspace(1e-6, 20, 5000, dtype=np.float32)
     lg = np.array([O.lib().orc_logf(float(x)) for x in xs])

@@ -25,7 +25,7 @@ import othello_mcts as om  # noqa: E402
 from othello_mcts.synthetic import alphazero_state_dict, live_state_dict  # noqa: E402
 
 NAMES = ["waves", "cycles", "descent", "levels", "leaves", "post", "backup", "backed_up", "terminal",
-         "max_cycles", "batches", "select", "expand", "path_w"]
+         "max_cycles", "batches", "select", "expand", "path_w", "noise", "refill"]
 moves = int(os.environ.get("MOVES", "64"))
 games = int(os.environ.get("GAMES", "256"))
 lib = ctypes.CDLL(str(ROOT / "othello-alphazero_amd" / "othello_mcts" / "liboamd.so"))
@@ -72,5 +72,5 @@ print(f"all: cycles/wave {tot['cycles'] / w:.0f}  descent {tot['descent'] / tot[
       f"post {tot['post'] / tot['cycles']:.3f}  backup {tot['backup'] / tot['cycles']:.3f} of wave cycles; "
       f"cycles/level {tot['descent'] / lv:.0f}, levels/leaf {tot['levels'] / lf:.2f}, post/leaf "
       f"{tot['post'] / lf:.0f}, backup/leaf {tot['backup'] / bu:.0f} (expansion {tot['expand'] / bu:.0f}, path "
-      f"statistics {tot['path_w'] / bu:.0f}), terminal leaves {tot['terminal'] / lf:.3f}, "
+      f"statistics {tot['path_w'] / bu:.0f}), root noise/leaf {tot['noise'] / lf:.0f} (refills {tot['refill'] / lf:.0f}), terminal leaves {tot['terminal'] / lf:.3f}, "
       f"longest wave {tot['max_cycles']}")
