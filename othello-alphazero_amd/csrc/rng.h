@@ -7,10 +7,10 @@
 //   stream_key(game_key, event, sub) -> uniform(stream_key, k), k = 0,1,...
 // One "event" per random decision of a game (a leaf's transform, a root
 // selection's noise vector, a move choice); "sub" separates the children of
-// one noise vector. The Gamma sampler and the log/exp it uses are written in
-// plain IEEE float operations (no libm, no FMA contraction: this file must be
-// compiled with -ffp-contract=off) so that host and device produce the same
-// bits. The test oracle (oracle/omcts_oracle.c) restates the same spec.
+// one noise vector. The Gamma sampler and the log/exp/cos^2 it uses are
+// written in plain IEEE float operations (no libm beyond the exact floorf, no
+// FMA contraction: this file must be compiled with -ffp-contract=off) so that
+// host and device produce the same bits. The test oracle (oracle/omcts_oracle.c) restates the same spec.
 #pragma once
 
 #include <hip/hip_runtime.h>
