@@ -444,7 +444,10 @@ struct oamd_engine {
         }
         while (n_events < nev) {
             const int k = n_events;
-            HIPCHK(hipEventCreateWithFlags(&sel_ev[k], hipEventDisableTiming));
+            // sel_ev only orders kernels of this device (the split schedule's tree
+            // operations): no system-scope fence (its host-visibility cache
+            // maintenance) on the cross-stream path of every round
+            HIPCHK(hipEventCreateWithFlags(&sel_ev[k], hipEventDisableTiming | hipEventDisableSystemFence));
             HIPCHK(hipEventCreateWithFlags(&nn_ev[k], hipEventDisableTiming));
             ++n_events;
         }
