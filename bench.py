@@ -907,7 +907,7 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     # rounds included; their count adapts per search) + the final backup
     rounds = m["rounds"] / m["searches"] if m.get("searches") else float(max_search_rounds(args))
     tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch), "rounds_per_search": round(rounds, 3),
-            "max_rounds_per_search": max_search_rounds(args)}
+            "max_rounds_per_search": max_search_rounds(args), "kernel_hash": kernel_hash("tree")}
     for name, ms, n in (("k_tree", m["select_ms"], m["tree_launches"]),
                         ("k_tree_final_backup", m["backup_ms"], m["final_launches"])):
         avg = ms / max(1, n)

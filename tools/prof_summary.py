@@ -160,6 +160,8 @@ def nn_summary(outdir: str, prefix: str, tag: str) -> dict:
 
 def bench_summary(outdir: str, prefix: str, tag: str) -> dict:
     dirs = [d for d in sorted(glob.glob(f"{outdir}/pmc_{prefix}_*")) if Path(d).is_dir()]
+    if not dirs:  # nothing to summarise: write nothing (the committed records stay)
+        raise SystemExit(f"prof_summary: no PMC passes {outdir}/pmc_{prefix}_*")
     by, durs = gather(dirs)
     c = {k: avg(v) for k, v in sorted(by.items())}
     bench = None
@@ -181,7 +183,9 @@ def bench_summary(outdir: str, prefix: str, tag: str) -> dict:
         launches = r.get("launches") or r.get("timed_region_launches")
         rows = (bench["work"]["n_eval"] / (launches * regular / rounds) if rounds and launches
                 else r.get("n_eval_per_launch", r["rows_per_launch"]))
-    fpr = bench["roofline"]["flops_per_row"] if bench else None
+    if not bench:
+        raise SystemExit(f"prof_summary: no bench line in the logs of {outdir}/pmc_{prefix}_*")
+    fpr = bench["roofline"]["flops_per_row"]
     res = {"tag": tag, "source": f"tools/gpu.sh pmc {prefix}_* over bench.py",
            "workload": bench["config"]["workload"] if bench else None,
            "passes": [Path(d).name for d in dirs], "dispatches_timed": len(durs),
@@ -195,22 +199,29 @@ def bench_summary(outdir: str, prefix: str, tag: str) -> dict:
                      "derived": derive(tc, avg(tdurs), None, None)}
     OUT.mkdir(exist_ok=True)
     (OUT / f"{tag}_bench_pmc.json").write_text(json.dumps(res, indent=1) + "\n")
-    sys.path.insert(0, str(ROOT))
-    from bench import kernel_hash  # noqa: E402  (the sources these passes ran)
+    # the kernel sources these passes ran: the hashes the bench line read from
+    # the library it loaded (not the sources on disk now)
+    resnet_hash = bench["roofline"]["kernel_hash"]
+    tree_hash = bench["tree_kernels"].get("kernel_hash")
+    if tree_hash is None:  # bench lines before the tree hash was recorded
+        sys.path.insert(0, str(ROOT))
+        from bench import kernel_hash  # noqa: E402
 
-    if "hbm_bytes_per_launch" in res["derived"] and bench:
+        tree_hash = kernel_hash("tree")
+
+    if "hbm_bytes_per_launch" in res["derived"]:
         (OUT / "traffic_resnet.json").write_text(json.dumps({
             "tag": tag, "bytes_per_launch": res["derived"]["hbm_bytes_per_launch"],
             "workload": bench["config"]["workload"], "rows_per_launch": bench["roofline"]["rows_per_launch"],
-            "kernel_hash": kernel_hash("resnet"),
+            "kernel_hash": resnet_hash,
             "note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> B) per k_resnet launch, rocprofv3 --pmc, separate passes "
                     "(tools/prof_summary.py)"}, indent=1) + "\n")
     td = res["k_tree"]["derived"]
-    if "hbm_bytes_per_launch" in td and bench:
+    if "hbm_bytes_per_launch" in td:
         (OUT / "traffic_tree.json").write_text(json.dumps({
             "tag": tag, "kernels": {"k_tree": {"bytes_per_launch": td["hbm_bytes_per_launch"],
                                                "avg_ms_rocprof": td.get("avg_launch_ms")}},
-            "workload": bench["config"]["workload"], "kernel_hash": kernel_hash("tree"),
+            "workload": bench["config"]["workload"], "kernel_hash": tree_hash,
             "note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> B) per k_tree launch (every round of a search, final "
                     "backups included), rocprofv3 --pmc, separate passes (tools/prof_summary.py)"},
             indent=1) + "\n")
