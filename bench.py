@@ -40,6 +40,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import socket
 import subprocess
 import sys
@@ -92,6 +93,40 @@ def max_search_rounds(args) -> int:
     extra = (min(args.chain_cuts, args.threads * steps // args.chain_budget)
              if (not args.round_robin_endgames and args.chain_budget > 0 and not single_game_split(args)) else 0)
     return steps + extra
+
+
+# SURVEY.md §8(d) "algorithmic bytes per simulation" of the tree kernels, per
+# item: a descent level reads its children's N, W, P (12 B each) and writes the
+# virtual loss (16 B RMW), the backup writes each level again (16 B RMW); an
+# expansion writes 28 B per created child + an 8 B child-range record; an NN
+# row gathers H x 16 B of history, writes (1 + 2H) x 8 B of bit-packed
+# features and reads back 65 x 2 + 2 B of policy / value.
+TREE_BYTES = {"per_child_scanned": 12, "per_level": 16 + 16, "per_expansion": 8, "per_child_created": 28}
+
+
+def tree_bytes_per_row(history: int) -> int:
+    return history * 16 + (1 + 2 * history) * 8 + 65 * 2 + 2
+
+
+def tree_algorithmic_bytes(work: dict, n_eval: int, history: int) -> dict:
+    """The tree kernels' algorithmic bytes (TREE_BYTES) over a window's
+    engine counters (oamd_engine_tree_work): total and per tree launch."""
+    b = (TREE_BYTES["per_child_scanned"] * work["children_scanned"] + TREE_BYTES["per_level"] * work["levels"]
+         + TREE_BYTES["per_expansion"] * work["expansions"]
+         + TREE_BYTES["per_child_created"] * work["children_created"] + tree_bytes_per_row(history) * n_eval)
+    return {"bytes": b, "per_launch": b / max(1, work["launches"])}
+
+
+def resnet_weight_bytes(in_ch: int, C: int, R: int, hidden: int, dtype_bytes: int = 2) -> int:
+    """Algorithmic weight bytes of one launch (BN folded): the 3x3 convolutions
+    in the compute dtype, biases and heads in fp32."""
+    convs = 9 * in_ch * C + 2 * R * 9 * C * C
+    small = (1 + 2 * R) * C + (C * 3 + 3) + (128 * 65 + 65) + (64 * hidden + hidden) + (hidden + 1)
+    return dtype_bytes * convs + 4 * small
+
+
+# per evaluated row: packed features in (2 + 2H words of 8 B at H = 8), fp32 policy (65) + value out
+RESNET_ROW_BYTES = (2 + 2 * 8) * 8 + 65 * 4 + 4
 
 
 def resnet_flops_per_eval(in_ch: int, C: int, R: int, hidden: int) -> float:
@@ -220,37 +255,70 @@ def grouped() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
-def timed_max(world: int, run, sync, device: str) -> tuple[float, float]:
+def cpu_seconds() -> float:
+    """Host CPU seconds (user + system) of this process, every thread."""
+    r = resource.getrusage(resource.RUSAGE_SELF)
+    return r.ru_utime + r.ru_stime
+
+
+def timed_max(world: int, run, sync, device: str) -> tuple[float, float, float]:
     """Run `run()` bracketed by barrier + device sync on both sides; return the
-    MAX wall time over ranks (the whole job's time) and this rank's own."""
+    MAX wall time over ranks (the whole job's time: barrier to barrier), this
+    rank's own time (its start barrier to its own final sync, before it waits
+    for the others: a slow rank shows here) and the host CPU seconds this
+    rank's process spent over its own time (getrusage)."""
     if grouped():
         dist.barrier()
     sync()
     t0 = time.perf_counter()
+    c0 = cpu_seconds()
     run()
     sync()
+    own = time.perf_counter() - t0
+    cpu = cpu_seconds() - c0
     if grouped():
         dist.barrier()
-    own = time.perf_counter() - t0
-    t = torch.tensor([own], dtype=torch.float64, device=device)
+    job = time.perf_counter() - t0
+    t = torch.tensor([job], dtype=torch.float64, device=device)
     if grouped():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item()), own
+    return float(t.item()), own, cpu
 
 
-def rank_table(world: int, rank: int, device_id: str, sims: int, own_s: float | None = None) -> list[dict]:
-    """[{rank, device, sims, ms, sims_per_s}] of every rank (all_gather_object
-    over the job's process group): which physical device each rank ran on, its
-    units and its own time over the barrier-bracketed region (the line's value
-    uses the MAX over ranks; a slow rank shows here)."""
+def rank_table(world: int, rank: int, device_id: str, sims: int, own_s: float | None = None,
+               cpu_s: float | None = None) -> list[dict]:
+    """[{rank, device, sims, ms, sims_per_s, cpu_s_per_s}] of every rank
+    (all_gather_object over the job's process group): which physical device
+    each rank ran on, its units, its own time (start barrier to its own final
+    sync; the line's value uses the MAX over ranks of the barrier-to-barrier
+    time, so a slow rank shows here) and the host CPU seconds its process used
+    per wall second of that time (the host budget: N ranks need N x this of
+    the box's CPUs)."""
     me = {"rank": rank, "device": device_id, "sims": sims}
     if own_s is not None:
         me["ms"] = round(own_s * 1e3, 3)
         me["sims_per_s"] = round(sims / own_s, 1)
+        if cpu_s is not None:
+            me["cpu_s_per_s"] = round(cpu_s / own_s, 3)
     if not grouped():
         return [me]
     out: list = [None] * world
     dist.all_gather_object(out, me)
+    return out
+
+
+def host_budget(ranks: list[dict]) -> dict:
+    """The host CPUs the ranks used over the timed region (rank_table's
+    cpu_s_per_s) against the CPUs this process may use (usable_cpus: the
+    cgroup quota of a GPU box). At the driver's N = 8 the node's ranks need
+    8 x the per-rank figure; `fits_8_ranks` compares that with the quota this
+    box grants one process (the 8-GPU node's own quota is not visible here)."""
+    per = [r["cpu_s_per_s"] for r in ranks if "cpu_s_per_s" in r]
+    cpus = usable_cpus()
+    out = {"usable_cpus": cpus["usable"], "cgroup_quota_cpus": cpus["cgroup_quota_cpus"], "ranks": len(ranks)}
+    if per:
+        out.update({"cpu_s_per_s_max": max(per), "cpu_s_per_s_sum": round(sum(per), 3),
+                    "need_at_8_ranks": round(8 * max(per), 2), "fits_8_ranks": bool(8 * max(per) <= cpus["usable"])})
     return out
 
 
@@ -511,13 +579,14 @@ class EngineWorkload:
         e = self.b.engine
         e.enable_timing(max(1, self.args.timing_every if every is None else every))
         self.t0 = (e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy(), e.round_counts(),
-                   e.descent_depths())
+                   e.descent_depths(), e.tree_work())
 
     def stop_measuring(self) -> dict:
         e = self.b.engine
-        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), (bu0, bl0), (sc0, ro0, fl0), (lv0, ds0, _) = self.t0
-        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), (bu1, bl1), (sc1, ro1, fl1), (lv1, ds1, dmax) = (
-            e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy(), e.round_counts(), e.descent_depths())
+        (ms0, la0, rw0), (se0, bk0, tl0), (si0, ev0), (bu0, bl0), (sc0, ro0, fl0), (lv0, ds0, _), tw0 = self.t0
+        (ms1, la1, rw1), (se1, bk1, tl1), (si1, ev1), (bu1, bl1), (sc1, ro1, fl1), (lv1, ds1, dmax), tw1 = (
+            e.nn_timing(), e.tree_timing(), e.work_counters(), e.nn_busy(), e.round_counts(), e.descent_depths(),
+            e.tree_work())
         overflow_games, depth_capped = e.status()
         if overflow_games or depth_capped:
             raise SystemExit(f"bench invalid: {overflow_games} game(s) overflowed their node pool, "
@@ -527,7 +596,9 @@ class EngineWorkload:
                 "backup_ms": bk1 - bk0, "tree_launches": tl1 - tl0, "final_launches": fl1 - fl0,
                 "searches": sc1 - sc0, "rounds": ro1 - ro0, "sims": si1 - si0, "evals": ev1 - ev0,
                 "overflow_games": overflow_games,
-                "depth_mean": (ds1 - ds0) / max(1, lv1 - lv0), "depth_max_since_start": dmax}
+                "depth_mean": (ds1 - ds0) / max(1, lv1 - lv0), "depth_max_since_start": dmax,
+                "tree_work": dict(zip(("levels", "children_scanned", "expansions", "children_created", "launches"),
+                                      (b - a for a, b in zip(tw0, tw1))))}
 
     def prior_stats(self, n: int = 256) -> dict:
         """The net's outputs on n real positions (the native kernel itself):
@@ -559,9 +630,11 @@ class EngineWorkload:
                 "policy_entropy_nats": round(float(-(p * np.log(np.maximum(p, 1e-30))).sum(1).mean()), 3)}
 
 
-def run_window(args, wl, world: int, backend: str, n: int, every: int | None = None) -> tuple[float, float, dict | None]:
+def run_window(args, wl, world: int, backend: str, n: int,
+               every: int | None = None) -> tuple[float, float, dict | None, float]:
     """n steps of `wl` in a barrier-bracketed region, the engine's counters
-    over it: (max-over-ranks seconds, this rank's seconds, measurements)."""
+    over it: (max-over-ranks seconds, this rank's seconds, measurements, this
+    rank's host CPU seconds)."""
     measuring = hasattr(wl, "start_measuring")
     if measuring:
         wl.start_measuring(every)
@@ -573,8 +646,8 @@ def run_window(args, wl, world: int, backend: str, n: int, every: int | None = N
             for _ in range(n):
                 wl.step()
 
-    dt_max, own = timed_max(world, run, wl.sync, "cuda" if backend == "nccl" else "cpu")
-    return dt_max, own, (wl.stop_measuring() if measuring else None)
+    dt_max, own, cpu = timed_max(world, run, wl.sync, "cuda" if backend == "nccl" else "cpu")
+    return dt_max, own, (wl.stop_measuring() if measuring else None), cpu
 
 
 def park_barrier(group) -> None:
@@ -599,16 +672,16 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
         for _ in range(args.warmup):
             wl.step()
     wl.sync()
-    dt_max, own, m = run_window(args, wl, world, backend, args.steps)
+    dt_max, own, m, cpu_s = run_window(args, wl, world, backend, args.steps)
     sustained = None
     if m is not None and args.sustained_moves > 0:
         # the engine's real workload: the same games played on through their
         # endgames (all-terminal batches, chain splitting) and restarts (the
         # roofline covers every launch; HIP events sample every 5th search)
-        dt_s, _, ms_ = run_window(args, wl, world, backend, args.sustained_moves)
+        dt_s, _, ms_, _ = run_window(args, wl, world, backend, args.sustained_moves)
         sustained = sustained_fields(args, ms_, world, sims_per_search, dt_s)
     value = aggregate_rate(world, args.games, sims_per_search, args.steps, dt_max)
-    ranks = rank_table(world, rank, wl.device_id, args.games * sims_per_search * args.steps, own)
+    ranks = rank_table(world, rank, wl.device_id, args.games * sims_per_search * args.steps, own, cpu_s)
     check_ranks(args, world, backend, ranks)
     n_devices = len({r["device"] for r in ranks})
     workload = (f"{args.games} concurrent self-play games per GPU, {args.sims} sims/move, "
@@ -665,6 +738,7 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
     }
     if args.dry_run:
         result["dry_run"] = True
+    result["host"] = host_budget(ranks)
     if m is not None:
         result.update(measured_fields(args, m, workload))
         result["net_outputs"] = wl.prior_stats()
@@ -717,7 +791,7 @@ def deep_tree_record(args, wl, world: int, rank: int, backend: str, sims_per_sea
     for name, n in (("from_openings", args.deep_tree_moves), ("sustained", args.sustained_moves)):
         if n <= 0:
             continue
-        dt, _, m = run_window(args, dw, world, backend, n, every=1)
+        dt, _, m, _ = run_window(args, dw, world, backend, n, every=1)
         a = copy.copy(args)
         a.steps = n  # the window's own moves (rows launched)
         mf = measured_fields(a, m, "")
@@ -762,7 +836,7 @@ def config_records(args, wl, world: int, rank: int, backend: str) -> dict:
     gc.collect()
     out = {}
     specs = (("configs3", "256x20b ResNet bf16, 256 games per GPU, 1600 sims/move (BASELINE configs[3])",
-              dict(channels=256, blocks=20, hidden=256, sims=1600, dtype="bf16", eval_batch=0, games=256), 2, 4),
+              dict(channels=256, blocks=20, hidden=256, sims=1600, dtype="bf16", eval_batch=0, games=256), 2, 10),
              ("configs4_shard", "128x10b ResNet fp16, 512 games per GPU, eval batch 2048, 800 sims/move "
               "(BASELINE configs[4]: 4096 games over 8 GPUs)",
               dict(channels=128, blocks=10, hidden=128, sims=800, dtype="fp16", eval_batch=2048, games=512), 2, 10))
@@ -773,7 +847,7 @@ def config_records(args, wl, world: int, rank: int, backend: str) -> dict:
         w = EngineWorkload(a, rank, wl.local, net_kind="live")
         w.steps(warm)
         w.sync()
-        dt, own, m = run_window(a, w, world, backend, n)
+        dt, own, m, _ = run_window(a, w, world, backend, n)
         L = a.threads * a.batch
         sps = L * ((a.sims + L - 1) // L)
         mf = measured_fields(a, m, "")
@@ -894,6 +968,10 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     tj = traffic_record("traffic_resnet.json", "resnet", workload)
     if tj and tj.get("rows_per_launch") == int(rows_per_launch):
         traffic = tj.get("bytes_per_launch")
+    # algorithmic bytes of one launch: the weights once + every evaluated row's
+    # features in and policy / value out
+    alg_nn = (resnet_weight_bytes(1 + 2 * args.history, args.channels, R, args.hidden)
+              + RESNET_ROW_BYTES * n_eval_per_launch)
     tree_bytes = {}
     tj = traffic_record("traffic_tree.json", "tree", workload)
     if tj:
@@ -908,14 +986,32 @@ def measured_fields(args, m: dict, workload: str) -> dict:
     rounds = m["rounds"] / m["searches"] if m.get("searches") else float(max_search_rounds(args))
     tree = {"bound": "latency", "sims_per_launch": int(rows_per_launch), "rounds_per_search": round(rounds, 3),
             "max_rounds_per_search": max_search_rounds(args), "kernel_hash": kernel_hash("tree")}
+    alg_tree = tree_algorithmic_bytes(m["tree_work"], m["evals"], args.history) if "tree_work" in m else None
     for name, ms, n in (("k_tree", m["select_ms"], m["tree_launches"]),
                         ("k_tree_final_backup", m["backup_ms"], m["final_launches"])):
         avg = ms / max(1, n)
         entry = {"avg_launch_ms": round(avg, 4)}
+        if name == "k_tree" and alg_tree is not None:
+            tw = m["tree_work"]
+            sims = max(1, m["sims"])
+            # every k_tree* launch of the window (select rounds, extra rounds,
+            # final backups, free-running rounds): the PMC record averages the same set
+            entry.update({"algorithmic_bytes_per_launch": round(alg_tree["per_launch"]),
+                          "algorithmic_bytes_per_sim": round(alg_tree["bytes"] / sims, 1),
+                          "byte_model": {"constants": TREE_BYTES, "per_nn_row": tree_bytes_per_row(args.history),
+                                         "window": tw,
+                                         "children_scanned_per_level": round(tw["children_scanned"]
+                                                                             / max(1, tw["levels"]), 3),
+                                         "children_per_expansion": round(tw["children_created"]
+                                                                         / max(1, tw["expansions"]), 3),
+                                         "source": "SURVEY.md §8(d) per-item bytes x the engine's counters "
+                                                   "(oamd_engine_tree_work) over the timed region"}})
         if name in tree_bytes:
             gbs = tree_bytes[name] / (avg * 1e-3) / 1e9
             entry.update({"hbm_bytes_per_launch": tree_bytes[name], "achieved_GB_s": round(gbs, 2),
                           "frac_hbm_peak": round(gbs / PEAK_HBM_GBS, 5)})
+            if "algorithmic_bytes_per_launch" in entry:
+                entry["counter_over_algorithmic"] = round(tree_bytes[name] / max(1.0, alg_tree["per_launch"]), 3)
         tree[name] = entry
     return {
         "overflow_games": m["overflow_games"],
@@ -931,6 +1027,8 @@ def measured_fields(args, m: dict, workload: str) -> dict:
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
+            "algorithmic_bytes_per_launch": round(alg_nn),
+            "traffic_over_algorithmic": round(traffic / alg_nn, 2) if traffic else None,
             "basis": ("n_eval rows (non-terminal leaves of every search and round in the timed region) per launch "
                       "x flops_per_row / busy ms per launch (the union of the kernel-recorded execution intervals "
                       "of every ResNet launch in the timed region / those launches)"),

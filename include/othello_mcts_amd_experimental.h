@@ -81,6 +81,16 @@ int oamd_debug_tree_stamps(uint64_t *out, int64_t n, int32_t reset);
  * lock-step. */
 int oamd_engine_set_free_running(oamd_engine *e, int32_t enable);
 
+/* Diagnostics: the tree kernels' algorithmic work since the engine was
+ * created (host outputs; waits for the engine's stream), the terms of the
+ * byte model of SURVEY.md §8(d) that bench.py prices per k_tree launch:
+ * descent levels (= the depth sum of oamd_engine_descent_depths), children
+ * whose statistics those levels scanned, expansions, children created, and
+ * tree kernel launches (k_tree, k_tree_wide, k_tree_free). Any pointer may be
+ * NULL. */
+int oamd_engine_tree_work(oamd_engine *e, int64_t *levels, int64_t *children_scanned, int64_t *expansions,
+                          int64_t *children_created, int64_t *launches);
+
 #ifdef __cplusplus
 }
 #endif

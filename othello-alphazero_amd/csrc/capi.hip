@@ -23,11 +23,12 @@
 using namespace oamd;
 
 constexpr int kMaxPipeline = 8;
-constexpr int kEvPerBlock = 4;
+constexpr int kEvPerBlock = 4;  // timing events per (round, group): tree begin/end, NN begin/end
 // device counters (k_tree): [0..1] sims / NN rows of the current search,
 // [2..3] cumulative, [4..5] of timed searches, [6] summed descent depths,
-// [7] deepest descent
-constexpr int kCounters = 8;  // timing events per (round, group): tree begin/end, NN begin/end
+// [7] deepest descent, [8..11] the tree work of oamd_engine_tree_work
+// (children scanned, expansions, children created, tree launches)
+constexpr int kCounters = 12;
 // Order of the pipeline groups' NN launches within an NN chain (one chain:
 // one after another, each owning every CU while the other groups' tree
 // kernels run beside it). OAMD_NN_ORDER 1: a token event passed between the
@@ -1491,6 +1492,20 @@ int oamd_engine_descent_depths(oamd_engine* e, int64_t* leaves, int64_t* depth_s
     return OAMD_OK;
 }
 
+int oamd_engine_tree_work(oamd_engine* e, int64_t* levels, int64_t* scanned, int64_t* expansions, int64_t* created,
+                          int64_t* launches) {
+    DeviceGuard dg(e->device);
+    unsigned long long c[kCounters] = {};
+    HIPCHK(hipMemcpyAsync(c, e->counters, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (levels) *levels = (int64_t)c[6];
+    if (scanned) *scanned = (int64_t)c[8];
+    if (expansions) *expansions = (int64_t)c[9];
+    if (created) *created = (int64_t)c[10];
+    if (launches) *launches = (int64_t)c[11];
+    return OAMD_OK;
+}
+
 int oamd_engine_set_pipeline(oamd_engine* e, int32_t groups) {
     if (groups < 0 || groups > kMaxPipeline)
         return fail(OAMD_INVALID_ARGUMENT, "pipeline groups must be in [0, " + std::to_string(kMaxPipeline) + "]");
@@ -1665,10 +1680,13 @@ int oamd_engine_selfplay_move(oamd_engine* e, const oamd_selfplay_config* cfg, i
 
 // Free-running self-play: n_moves moves of every game, each game on its own
 // (tree.hip k_tree_free). Rounds are enqueued in chunks: one per move's worth
-// of rounds (steps + 1 for the first search, steps for each later one: no game
-// can finish sooner), then tail chunks of kFreeTailRounds rounds until the
-// group's remaining-games counter, copied to pinned memory after every chunk
-// and read two chunks late (so the read never drains the queue), is 0. The
+// of rounds (steps + 1 for the first search, steps for each later one: a
+// schedule estimate only — a search whose batches are all terminal can
+// re-select several times in one round and finish sooner, and such a game
+// simply plays its next move in the same call), then tail chunks of
+// kFreeTailRounds rounds until the group's remaining-games counter, copied to
+// pinned memory after every chunk and read two chunks late (so the read never
+// drains the queue), is 0. The
 // tail chunks' ResNet launches use the small looping grid (extra_grid): only
 // lagging games have rows then. Returns once the last chunk is enqueued.
 static int selfplay_steps_free(oamd_engine* e, oamd_net* net, const oamd_selfplay_config* cfg, int n_moves,

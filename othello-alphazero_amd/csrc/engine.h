@@ -79,7 +79,7 @@ struct EngineView {
     float* value;    // G*L
     const float* explore_tab;  // kExploreTab
     float c_base, c_init, eps, alpha;
-    unsigned long long* counters;  // [0] sims, [1] evals (this search), [2] sims, [3] evals (cumulative)
+    unsigned long long* counters;  // [0..11], tree.hip add_counters / count_launch
     int32_t* rowlist;  // G*L: evaluation lists (pipeline group k: from its first game's row)
     int32_t* tstate;   // G*L (entry g*L + t for virtual thread t): batches selected | kTstatePend
     int32_t steps;     // batches per virtual thread and search: ceil(num_simulations / L)

@@ -718,6 +718,11 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
             int64_t launches;
             check(oamd_engine_tree_timing(e.h, &sel, &bk, &launches));
             return py::make_tuple(sel, bk, launches);
+        })
+        .def("tree_work", [](Engine& e) {
+            int64_t lv = 0, sc = 0, ex = 0, cr = 0, la = 0;
+            check(oamd_engine_tree_work(e.h, &lv, &sc, &ex, &cr, &la));
+            return py::make_tuple(lv, sc, ex, cr, la);
         });
 
     // GPU bitboard kernels over device buffers (data_ptr ints) for parity tests

@@ -287,7 +287,8 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
                                              int i0, int i1, uint64_t& event, int hist_node,
                                              int hist_n, unsigned long long& sims,
                                              unsigned long long& evals, int* cnt, int list_base,
-                                             unsigned long long& depth_sum, int& depth_max) {
+                                             unsigned long long& depth_sum, int& depth_max,
+                                             unsigned long long& scan_sum) {
     const int lane = lane_id();
     const int root = gs->root;
     const uint64_t key = gs->key;
@@ -328,6 +329,7 @@ __device__ __forceinline__ void select_range(const EngineView& E, int g, GameSta
         // exploration rate come from its lane (readlane), not from a second load.
         while (!(lk.player == 0 || lk.n_children == 0) && d < kMaxDepth - 1) {
             const int nc = lk.n_children, fc = lk.first_child;
+            scan_sum += (unsigned long long)nc;  // children whose stats this level reads
             int4 cs4 = make_int4(0, 0, 0, 0), cl4 = make_int4(0, 0, 0, 0);
             if (lane < nc) {
                 cs4 = *reinterpret_cast<const int4*>(E.stat + base + fc + lane);
@@ -568,7 +570,7 @@ __device__ __forceinline__ void expand_quads(const EngineView& E, size_t base, i
 // Expansion + backup of leaves [i0, i1) (search_thread.cpp:116-127, 130-190).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t base, int i0, int i1,
-                                             int& count, bool& overflow) {
+                                             int& count, bool& overflow, unsigned& expansions) {
     const int lane = lane_id();
     TS_T(tb0);
     TS_ADD(kTsBackedUp, i1 - i0);
@@ -637,6 +639,7 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
                 } else {
                     const int fc = count;
                     count += nc;
+                    ++expansions;
                     if (P.legal) {
                         expand_quads(E, base, leaf, P, fc, nc, t, polj);
                     } else if (lane == 0) {  // the pass: one child (position.h:382-386)
@@ -730,7 +733,9 @@ __device__ __forceinline__ void backup_range(const EngineView& E, int g, size_t 
 // Per-wave work counters of one k_tree launch.
 struct RoundAcc {
     unsigned long long sims = 0, evals = 0, depth_sum = 0;
+    unsigned long long scan_sum = 0;  // children scanned over every descent level
     int depth_max = 0;
+    unsigned expansions = 0;          // leaves expanded (children = the node count's growth)
 };
 
 // One round of game g's search schedule (see k_tree): virtual threads
@@ -763,7 +768,7 @@ __device__ __forceinline__ bool search_round(const EngineView& E, int g, GameSta
         int sel = st & kTstateSel;
         bool pend = (st & kTstatePend) != 0;
         if (do_backup && pend) {
-            backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
+            backup_range(E, g, base, t * B, (t + 1) * B, count, overflow, acc.expansions);
             pend = false;
         }
         // the thread's next batch; one whose leaves are all terminal needs no NN
@@ -782,7 +787,7 @@ __device__ __forceinline__ bool search_round(const EngineView& E, int g, GameSta
             const unsigned long long ev0 = acc.evals;
             TS_T(tsel0);
             select_range(E, g, gs, base, t * B, (t + 1) * B, event, hist_node, hist_n, acc.sims, acc.evals, cnt_add,
-                         list_base, acc.depth_sum, acc.depth_max);
+                         list_base, acc.depth_sum, acc.depth_max, acc.scan_sum);
             TS_T(tsel1);
             TS_ADD(kTsSelect, tsel1 - tsel0);
             TS_ADD(kTsBatches, 1);
@@ -790,7 +795,7 @@ __device__ __forceinline__ bool search_round(const EngineView& E, int g, GameSta
             if (acc.evals != ev0 || !E.terminal_skip) {
                 pend = true;
             } else {
-                backup_range(E, g, base, t * B, (t + 1) * B, count, overflow);
+                backup_range(E, g, base, t * B, (t + 1) * B, count, overflow, acc.expansions);
                 again = true;
                 ++chain;
 #if OAMD_CHAIN_PRIO > 0
@@ -811,21 +816,37 @@ __device__ __forceinline__ bool search_round(const EngineView& E, int g, GameSta
 // asks for them), [2..3] cumulative since the engine was created
 // (oamd_engine_work_counters), [4..5] the searches that record timing events,
 // [6] descent depths summed over every selected leaf, [7] the deepest descent
-// (levels below the root; oamd_engine_descent_depths)
-__device__ __forceinline__ void add_counters(const EngineView& E, const RoundAcc& acc, bool timed) {
+// (levels below the root; oamd_engine_descent_depths), and the tree kernels'
+// algorithmic work (oamd_engine_tree_work): [8] children scanned over every
+// descent level, [9] expansions, [10] children created, [11] tree launches
+// (lane 0 of each launch's first wave). children: the game's node count
+// growth this round (count_grown, no restart in between).
+__device__ __forceinline__ void add_counters(const EngineView& E, const RoundAcc& acc, bool timed,
+                                             unsigned children) {
     if (!E.counters) return;
-    atomicAdd(E.counters + 0, acc.sims);
-    atomicAdd(E.counters + 1, acc.evals);
-    atomicAdd(E.counters + 2, acc.sims);
-    atomicAdd(E.counters + 3, acc.evals);
-    if (timed) {
-        atomicAdd(E.counters + 4, acc.sims);
-        atomicAdd(E.counters + 5, acc.evals);
-    }
     if (acc.sims) {
+        atomicAdd(E.counters + 0, acc.sims);
+        atomicAdd(E.counters + 1, acc.evals);
+        atomicAdd(E.counters + 2, acc.sims);
+        atomicAdd(E.counters + 3, acc.evals);
+        if (timed) {
+            atomicAdd(E.counters + 4, acc.sims);
+            atomicAdd(E.counters + 5, acc.evals);
+        }
         atomicAdd(E.counters + 6, acc.depth_sum);
         atomicMax(E.counters + 7, (unsigned long long)acc.depth_max);
+        atomicAdd(E.counters + 8, acc.scan_sum);
     }
+    if (acc.expansions) {
+        atomicAdd(E.counters + 9, (unsigned long long)acc.expansions);
+        atomicAdd(E.counters + 10, (unsigned long long)children);
+    }
+}
+
+// counter [11]: one per tree launch (lane 0 of its first wave, before any
+// early return of an inactive game)
+__device__ __forceinline__ void count_launch(const EngineView& E) {
+    if (E.counters && blockIdx.x == 0 && lane_id() == 0) atomicAdd(E.counters + 11, 1ULL);
 }
 
 __device__ __forceinline__ void tree_round_kernel(const EngineView& E, int g0, int do_backup, int do_select, int t0,
@@ -834,6 +855,7 @@ __device__ __forceinline__ void tree_round_kernel(const EngineView& E, int g0, i
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
+    count_launch(E);
     // cuts_out (adaptive extra rounds, capi.hip): [0] the most cuts any game
     // of the launch's group used in this search, [1] the fewest empty squares
     // of an active game's root; reset by the search's first round, set by its
@@ -869,6 +891,7 @@ __device__ __forceinline__ void tree_round_kernel(const EngineView& E, int g0, i
     const int hist_node = lane < 16 ? gs->hist[lane] : -1;
     RoundAcc acc;
     int count = gs->count;
+    const int count0 = count;
     bool overflow = false;
     const int rp = budget > 0 && !fresh ? gs->resume : t0;  // this round's first thread
     int cuts = budget > 0 && !fresh ? gs->cuts : 0;
@@ -903,7 +926,7 @@ __device__ __forceinline__ void tree_round_kernel(const EngineView& E, int g0, i
             }
         }
 #endif
-        if (do_select) add_counters(E, acc, timed != 0);
+        add_counters(E, acc, timed != 0, (unsigned)(count - count0));
     }
 }
 
@@ -1336,6 +1359,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     const int g = g0 + (int)blockIdx.x;
     const int lane = lane_id();
     if (cnt_reset && blockIdx.x == 0 && lane == 0) *cnt_reset = 0;
+    count_launch(E);
     GameState* gs = E.games + g;
     const size_t base = (size_t)g * E.cap;
     int moves = gs->moves_left;
@@ -1346,6 +1370,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
     int hist_n = gs->hist_n;
     int hist_node = lane < 16 ? gs->hist[lane] : -1;
     int count = gs->count;
+    unsigned grown = 0;  // children created (the node count restarts with a finished game)
+    int count0 = count;
     bool overflow = false;
     RoundAcc acc;
     int rp = fresh || budget <= 0 ? 0 : gs->resume;
@@ -1365,6 +1391,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
             if (overflow) atomicOr(&gs->flags, (int)kOverflow);
         }
         overflow = false;
+        grown += (unsigned)(count - count0);
         __builtin_amdgcn_wave_barrier();
         wait_stores();
         const size_t slot = per_move ? (size_t)(n_moves - moves) * E.G : 0;
@@ -1378,6 +1405,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
         hist_n = gs->hist_n;
         hist_node = lane < 16 ? gs->hist[lane] : -1;
         count = gs->count;
+        count0 = count;
         rp = 0;
         cuts = 0;
         cut_at = -1;
@@ -1394,7 +1422,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(48))) void k_tre
         gs->count = count;
         if (overflow) atomicOr(&gs->flags, (int)kOverflow);
         if (moves == 0 && remaining) atomicSub(remaining, 1);
-        add_counters(E, acc, timed != 0);
+        add_counters(E, acc, timed != 0, grown + (unsigned)(count - count0));
     }
 }
 

@@ -41,31 +41,49 @@ def _one_line(r) -> dict:
     return json.loads(lines[0])
 
 
-def _check_two_rank_line(out: dict, steps: int, step_ms: float, games: int) -> None:
+def _check_line(out: dict, world: int, steps: int, step_ms: float, games: int) -> None:
     assert out["dry_run"] is True and "DRY RUN" in out["data"]
     assert out["metric"].startswith("MCTS simulations/sec (whole node)")
-    assert out["n_gpus"] == 2 and out["steps"] == steps and out["scaling"] == "weak"
+    assert out["n_gpus"] == world and out["steps"] == steps and out["scaling"] == "weak"
     ranks = sorted(out["config"]["ranks"], key=lambda r: r["rank"])
-    assert [r["rank"] for r in ranks] == [0, 1]
-    assert len({r["device"] for r in ranks}) == 2
+    assert [r["rank"] for r in ranks] == list(range(world))
+    assert len({r["device"] for r in ranks}) == world
     assert all(r["sims"] == games * 800 * steps for r in ranks)
-    # per-rank time and rate: rank 1 sleeps twice as long
+    # per-rank time and rate: rank r sleeps (1 + r) x step_ms
+    # per step. A rank's own time stops at its own final sync, before it waits
+    # for the slower ranks at the closing barrier: rank 0 must NOT
+    # read the slowest rank's time
     assert all(r["ms"] > 0 and abs(r["sims_per_s"] - r["sims"] / (r["ms"] / 1e3)) <= 1e-3 * r["sims_per_s"] + 0.1
                for r in ranks)
-    assert ranks[1]["ms"] >= steps * 2 * step_ms and ranks[0]["ms"] >= steps * step_ms
-    # the max over ranks: rank 1 sleeps 2 x step_ms per step
+    for r in ranks:
+        assert r["ms"] >= steps * (1 + r["rank"]) * step_ms
+    assert ranks[0]["ms"] < 1.5 * steps * step_ms + 30.0
+    assert ranks[-1]["ms"] > ranks[0]["ms"] + (world - 1) * steps * step_ms * 0.5
+    # host budget: CPU seconds per wall second of each
+    # rank's timed region; a sleeping dry-run rank uses almost none
+    assert all(0.0 <= r["cpu_s_per_s"] < 0.5 for r in ranks)
+    host = out["host"]
+    assert host["ranks"] == world and host["usable_cpus"] >= 1
+    assert host["cpu_s_per_s_max"] == max(r["cpu_s_per_s"] for r in ranks)
+    assert host["need_at_8_ranks"] == round(8 * host["cpu_s_per_s_max"], 2)
+    # the max over ranks: the last rank sleeps world x step_ms per step
     dt = out["ms_per_step"] * steps / 1e3
-    assert dt >= steps * 2 * step_ms / 1e3
-    # whole-job rate = both ranks' units / the max time
-    assert abs(out["value"] - 2 * games * 800 * steps / dt) <= 1e-3 * out["value"] + 0.1
+    assert dt >= steps * world * step_ms / 1e3
+    assert dt * 1e3 >= max(r["ms"] for r in ranks)
+    # whole-job rate = every rank's units / the max time
+    assert abs(out["value"] - world * games * 800 * steps / dt) <= 1e-3 * out["value"] + 0.1
     assert "REHEARSAL" not in out["config"]["parallelism"] and out["config"]["backend"] == "gloo"
     assert "roofline" not in out
     # the CPU baseline rides on every world size's line (rank 0, after the
     # timed regions, the other ranks parked at a gloo barrier); a dry run
     # times one move of it
     cb = out["cpu_baseline"]
-    assert cb["world_size"] == 2 and cb["moves"] == 1 and cb["value"] > 0 and cb["kind"] == "port"
+    assert cb["world_size"] == world and cb["moves"] == 1 and cb["value"] > 0 and cb["kind"] == "port"
     assert "dry run" in cb["note"]
+
+
+def _check_two_rank_line(out: dict, steps: int, step_ms: float, games: int) -> None:
+    _check_line(out, 2, steps, step_ms, games)
 
 
 def test_bare_bench_gpus2_starts_its_own_ranks():
@@ -81,6 +99,17 @@ def test_driver_launch_gpus2():
               "--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "0", "--games", "8", "--dry-step-ms", "25"])
     assert "starting" not in r.stderr  # under a launcher bench.py starts nothing itself
     _check_two_rank_line(_one_line(r), 2, 25.0, 8)
+
+
+def test_driver_launch_gpus8_dry_run():
+    """the driver's N = 8 launch, rehearsed on the CPU: 8
+    gloo ranks, the rank table, the MAX reduction (rank 7 is the slowest), the
+    aggregate rate, the host budget and the CPU baseline at world size 8."""
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+              "--master-addr=127.0.0.1", f"--master-port={_free_port()}", BENCH,
+              "--gpus", "8", "--dry-run", "--steps", "2", "--warmup", "0", "--games", "256", "--dry-step-ms", "15"],
+             timeout=600)
+    _check_line(_one_line(r), 8, 2, 15.0, 256)
 
 
 def test_driver_launch_gpus1_joins_a_process_group():
@@ -123,8 +152,8 @@ def test_single_rank_helpers():
     assert bench.shard_seeds(2025, 0) != bench.shard_seeds(2025, 1)
     assert bench.aggregate_rate(8, 256, 800, 10, 2.0) == 8 * 256 * 800 * 10 / 2.0
     calls = []
-    dt, own = bench.timed_max(1, lambda: calls.append(1), lambda: calls.append(0), "cpu")
-    assert calls == [0, 1, 0] and dt >= 0.0 and own == dt
+    dt, own, cpu = bench.timed_max(1, lambda: calls.append(1), lambda: calls.append(0), "cpu")
+    assert calls == [0, 1, 0] and dt >= own >= 0.0 and cpu >= 0.0
     cpus = bench.usable_cpus()
     assert 1 <= cpus["usable"] <= cpus["nproc"]
     cmd = bench.launch_command(4, ["--gpus", "4"], 1234)
