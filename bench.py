@@ -432,6 +432,9 @@ def parse_args(argv: list[str]):
     ap.add_argument("--timing-every", type=int, default=5,
                     help="record the kernels' HIP events on every N-th timed search (1 = all; the event "
                          "packets add ~10 us per NN launch boundary to the searches they time)")
+    ap.add_argument("--spin-sync", action="store_true",
+                    help="end the timed region with a plain torch.cuda.synchronize() (spins a host CPU) instead of a "
+                         "blocking-sync event wait first")
     ap.add_argument("--dry-run", action="store_true",
                     help="rank plumbing only: no GPU, no search (gloo, each step a fixed sleep)")
     ap.add_argument("--dry-step-ms", type=float, default=20.0, help="--dry-run: ms per step (rank r: x (1 + r))")
@@ -573,6 +576,14 @@ class EngineWorkload:
                                   keep_all=False)
 
     def sync(self) -> None:
+        """torch.cuda.synchronize(), preceded by a wait on a blocking-sync event
+        of the stream the engine joins its pipeline groups into (the host
+        thread sleeps instead of spinning a CPU through the timed region;
+        --spin-sync: the plain synchronize)."""
+        if not self.args.spin_sync:
+            ev = torch.cuda.Event(blocking=True)
+            ev.record()
+            ev.synchronize()
         torch.cuda.synchronize()
 
     def start_measuring(self, every: int | None = None) -> None:

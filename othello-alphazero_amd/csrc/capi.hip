@@ -23,6 +23,19 @@
 using namespace oamd;
 
 constexpr int kMaxPipeline = 8;
+
+// Events the host waits on for a readback (the adaptive extra rounds' cut
+// counts, the free-running call's remaining-games counters): blocking sync,
+// so a waiting host thread sleeps instead of spinning a CPU. The reads are
+// two chunks late, off the GPU's critical path, so the wake-up latency is
+// hidden; the host budget of 8 ranks on one node is what it saves (bench.py
+// rank table cpu_s_per_s). OAMD_SPIN_SYNC=1: spinning waits
+// (A/B only).
+static unsigned readback_event_flags() {
+    const char* v = std::getenv("OAMD_SPIN_SYNC");
+    const bool spin = v && v[0] == '1';
+    return hipEventDisableTiming | (spin ? 0u : (unsigned)hipEventBlockingSync);
+}
 constexpr int kEvPerBlock = 4;  // timing events per (round, group): tree begin/end, NN begin/end
 // device counters (k_tree): [0..1] sims / NN rows of the current search,
 // [2..3] cumulative, [4..5] of timed searches, [6] summed descent depths,
@@ -212,7 +225,7 @@ struct oamd_engine {
             rc = fail(OAMD_RUNTIME, "cut slots: hipHostMalloc failed");
         for (auto& row : evs)
             for (auto& x : row)
-                if (!rc && hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
+                if (!rc && hipEventCreateWithFlags(&x, readback_event_flags()) != hipSuccess)
                     rc = fail(OAMD_RUNTIME, "cut slots: hipEventCreate failed");
         if (rc) {
             for (auto& row : evs)
@@ -247,7 +260,7 @@ struct oamd_engine {
             rc = fail(OAMD_RUNTIME, "free-running slots: hipHostMalloc failed");
         for (auto& row : evs)
             for (auto& x : row)
-                if (!rc && hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
+                if (!rc && hipEventCreateWithFlags(&x, readback_event_flags()) != hipSuccess)
                     rc = fail(OAMD_RUNTIME, "free-running slots: hipEventCreate failed");
         if (rc) {
             for (auto& row : evs)

@@ -568,3 +568,30 @@ def test_more_than_65535_batches_per_thread(om):
         assert info["visit_count"] == 70000
         assert sum(info["visit_counts"]) == 70000 - 1  # the first leaf is the unexpanded root
     assert b.engine.status() == (0, 0)
+
+
+def test_tree_work_counters_price_the_byte_model(om):
+    """the counters bench.py prices with SURVEY §8(d)'s
+    per-item bytes (oamd_engine_tree_work) count what the tree kernels did:
+    levels = the summed descent depths, children created = the games' node
+    count growth, an expansion creates >= 1 child and needs an evaluated
+    leaf, every descent level scans >= 1 child, one count per tree launch."""
+    from othello_mcts.synthetic import live_state_dict
+
+    net = om.NativeNet(live_state_dict(5, 17, 128, 2, 32), device=0)
+    b = _engine(om, 64, 8, 256, 41)
+    nodes0 = sum(b.root_info(g)["node_count"] for g in range(64))
+    lv0, sc0, ex0, cr0, la0 = b.engine.tree_work()
+    _, ds0, _ = b.engine.descent_depths()
+    sims, evals = b.search(net)
+    lv1, sc1, ex1, cr1, la1 = b.engine.tree_work()
+    _, ds1, _ = b.engine.descent_depths()
+    nodes1 = sum(b.root_info(g)["node_count"] for g in range(64))
+    assert lv1 - lv0 == ds1 - ds0 > 0
+    assert cr1 - cr0 == nodes1 - nodes0 > 0
+    assert 0 < ex1 - ex0 <= evals and ex1 - ex0 <= cr1 - cr0
+    assert sc1 - sc0 >= lv1 - lv0
+    steps = 256 // 32
+    assert la1 - la0 >= steps  # >= one launch per round (2 pipeline groups: 2 per round + final backups)
+    numerics.record("tree work counters", f"levels={lv1 - lv0} scanned={sc1 - sc0} expansions={ex1 - ex0} "
+                                          f"children={cr1 - cr0} launches={la1 - la0} sims={sims} evals={evals}")
