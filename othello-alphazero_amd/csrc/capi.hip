@@ -245,6 +245,9 @@ struct oamd_engine {
     // rounds until every group's remaining-games counter (read back two chunks
     // late, pinned memory behind events) is 0
     bool free_running = true;
+    // base chunks wait for the chunk two back before they are enqueued
+    // (OAMD_SPIN_SYNC=1: no wait, A/B only)
+    bool throttle_enqueue = !(std::getenv("OAMD_SPIN_SYNC") && std::getenv("OAMD_SPIN_SYNC")[0] == '1');
     static constexpr int kFreeSlots = 4;
     static constexpr int kFreeTailRounds = 4;
     int32_t* remaining_dev = nullptr;   // [kMaxPipeline]
@@ -1736,6 +1739,15 @@ static int selfplay_steps_free(oamd_engine* e, oamd_net* net, const oamd_selfpla
             const bool tail = round >= base_rounds;
             if (!tail) {
                 R = (int)std::min<int64_t>(round == 0 ? steps + 1 : steps, base_rounds - round);
+                // keep at most two chunks (~two moves of GPU work) queued ahead:
+                // wait (blocking, the thread sleeps) for chunk - 2 to finish.
+                // Enqueuing every move at once filled the hardware queues and
+                // the host spun a CPU in the launch calls for the whole call
+                // (host budget)
+                if (chunk >= 2 && e->throttle_enqueue) {
+                    const int slot = (int)((chunk - 2) % oamd_engine::kFreeSlots);
+                    for (int k = 0; k < K; ++k) HIPCHK(hipEventSynchronize(e->free_ev[slot][k]));
+                }
             } else {
                 if (chunk >= 2) {  // chunk - 2's readback: done by now while chunk - 1 is queued
                     const int slot = (int)((chunk - 2) % oamd_engine::kFreeSlots);

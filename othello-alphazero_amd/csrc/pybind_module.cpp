@@ -437,7 +437,7 @@ private:
     std::string torch_device_;
     bool pin_;
     bool native_ = true;
-    std::string nn_dtype_ = "bf16";
+    std::string nn_dtype_ = "fp16";
     int device_ = 0;
     std::unique_ptr<Engine> engine_;
 };
@@ -491,7 +491,7 @@ PYBIND11_MODULE(_othello_mcts_impl, m) {
              "history_size"_a = 4, "torch_device"_a = "cpu", "torch_pin_memory"_a = false,
              "num_simulations"_a = 800, "num_threads"_a = 2, "batch_size"_a = 16, "c_puct_base"_a = 20000.0f,
              "c_puct_init"_a = 2.5f, "dirichlet_epsilon"_a = 0.25f, "dirichlet_alpha"_a = 0.5f,
-             "node_capacity"_a = 0, "seed"_a = 0, "native_nn"_a = true, "nn_dtype"_a = "bf16")
+             "node_capacity"_a = 0, "seed"_a = 0, "native_nn"_a = true, "nn_dtype"_a = "fp16")
         .def("reset_position", &MCTS::reset_position)
         .def("position", &MCTS::position)
         .def("search", &MCTS::search)

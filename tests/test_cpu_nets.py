@@ -112,3 +112,18 @@ def test_live_state_dict_is_deterministic_and_keyed_like_the_reference():
     assert (f["residual_blocks.1.norm2.weight"][:2] == 0).all() and (f["residual_blocks.1.norm2.bias"][:2] == 0).all()
     with pytest.raises(ValueError):
         live_state_dict(3, 9, 128, 2, 32, policy="nope")
+
+
+def test_fp16_headroom_of_the_drop_in_default():
+    """The drop-in MCTS converts a module to fp16 only with FP16_HEADROOM (16x)
+    below the fp16 maximum on real positions (othello_mcts.native, round 6):
+    the trained and benched nets have thousands of x; a net whose activations
+    would overflow fp16 has none and is evaluated in bf16."""
+    from othello_mcts.native import FP16_HEADROOM, fp16_headroom
+    from othello_mcts.synthetic import live_state_dict, selfplay_state_dict
+
+    assert fp16_headroom(selfplay_state_dict(), 8) > 1000 * FP16_HEADROOM / 16
+    live = live_state_dict(2025, 17, 128, 9, 128)
+    assert fp16_headroom(live, 8) > 100
+    blown = {k: (v * 300 if k.endswith("conv2.weight") else v) for k, v in live.items()}
+    assert fp16_headroom(blown, 8) < FP16_HEADROOM
