@@ -576,14 +576,16 @@ class EngineWorkload:
                                   keep_all=False)
 
     def sync(self) -> None:
-        """torch.cuda.synchronize(), preceded by a wait on a blocking-sync event
-        of the stream the engine joins its pipeline groups into (the host
-        thread sleeps instead of spinning a CPU through the timed region;
-        --spin-sync: the plain synchronize)."""
+        """torch.cuda.synchronize(), preceded by polling an event of the stream
+        the engine joins its pipeline groups into, 100 us sleeps between polls
+        (the host thread sleeps instead of spinning a CPU through the timed
+        region; the poll adds <= 0.1 ms to it; --spin-sync: the plain
+        synchronize)."""
         if not self.args.spin_sync:
-            ev = torch.cuda.Event(blocking=True)
+            ev = torch.cuda.Event()
             ev.record()
-            ev.synchronize()
+            while not ev.query():
+                time.sleep(1e-4)
         torch.cuda.synchronize()
 
     def start_measuring(self, every: int | None = None) -> None:

@@ -5,11 +5,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/othello_mcts_amd.h"
@@ -24,17 +26,31 @@ using namespace oamd;
 
 constexpr int kMaxPipeline = 8;
 
-// Events the host waits on for a readback (the adaptive extra rounds' cut
-// counts, the free-running call's remaining-games counters): blocking sync,
-// so a waiting host thread sleeps instead of spinning a CPU. The reads are
-// two chunks late, off the GPU's critical path, so the wake-up latency is
-// hidden; the host budget of 8 ranks on one node is what it saves (bench.py
-// rank table cpu_s_per_s). OAMD_SPIN_SYNC=1: spinning waits
-// (A/B only).
+// Host waits for a readback (the adaptive extra rounds' cut counts, the
+// free-running call's remaining-games counters and its enqueue throttle):
+// off the GPU's critical path (the reads are two chunks late), so the thread
+// polls the event and sleeps 100 us between polls instead of spinning a CPU
+// in hipEventSynchronize (which spins here even on blocking-sync events:
+// bench.py's rank table read 1.0 CPU-s per s either way). The host budget of
+// 8 ranks on one node is what it saves (cpu_s_per_s).
+// OAMD_SPIN_SYNC=1: hipEventSynchronize (A/B only).
+static bool spin_sync() {
+    static const bool spin = [] {
+        const char* v = std::getenv("OAMD_SPIN_SYNC");
+        return v && v[0] == '1';
+    }();
+    return spin;
+}
 static unsigned readback_event_flags() {
-    const char* v = std::getenv("OAMD_SPIN_SYNC");
-    const bool spin = v && v[0] == '1';
-    return hipEventDisableTiming | (spin ? 0u : (unsigned)hipEventBlockingSync);
+    return hipEventDisableTiming | (spin_sync() ? 0u : (unsigned)hipEventBlockingSync);
+}
+static hipError_t host_wait(hipEvent_t ev) {
+    if (spin_sync()) return hipEventSynchronize(ev);
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q != hipErrorNotReady) return q;
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
 }
 constexpr int kEvPerBlock = 4;  // timing events per (round, group): tree begin/end, NN begin/end
 // device counters (k_tree): [0..1] sims / NN rows of the current search,
@@ -247,7 +263,7 @@ struct oamd_engine {
     bool free_running = true;
     // base chunks wait for the chunk two back before they are enqueued
     // (OAMD_SPIN_SYNC=1: no wait, A/B only)
-    bool throttle_enqueue = !(std::getenv("OAMD_SPIN_SYNC") && std::getenv("OAMD_SPIN_SYNC")[0] == '1');
+    bool throttle_enqueue = !spin_sync();
     static constexpr int kFreeSlots = 4;
     static constexpr int kFreeTailRounds = 4;
     int32_t* remaining_dev = nullptr;   // [kMaxPipeline]
@@ -1190,7 +1206,7 @@ static int pick_extra_rounds(oamd_engine* e, int* X) {
     if (q >= 0 && e->cut_x[s] >= 0) {
         int used = 0, empties = 64;
         for (int k = 0; k < e->cut_groups[s]; ++k) {
-            HIPCHK(hipEventSynchronize(e->cuts_ev[s][k]));
+            HIPCHK(host_wait(e->cuts_ev[s][k]));
             used = std::max(used, (int)e->cuts_host[2 * (s * kMaxPipeline + k)]);
             empties = std::min(empties, (int)e->cuts_host[2 * (s * kMaxPipeline + k) + 1]);
         }
@@ -1746,14 +1762,14 @@ static int selfplay_steps_free(oamd_engine* e, oamd_net* net, const oamd_selfpla
                 // (host budget)
                 if (chunk >= 2 && e->throttle_enqueue) {
                     const int slot = (int)((chunk - 2) % oamd_engine::kFreeSlots);
-                    for (int k = 0; k < K; ++k) HIPCHK(hipEventSynchronize(e->free_ev[slot][k]));
+                    for (int k = 0; k < K; ++k) HIPCHK(host_wait(e->free_ev[slot][k]));
                 }
             } else {
                 if (chunk >= 2) {  // chunk - 2's readback: done by now while chunk - 1 is queued
                     const int slot = (int)((chunk - 2) % oamd_engine::kFreeSlots);
                     for (int k = 0; k < K; ++k) {
                         if (gdone[k]) continue;
-                        HIPCHK(hipEventSynchronize(e->free_ev[slot][k]));
+                        HIPCHK(host_wait(e->free_ev[slot][k]));
                         if (e->remaining_host[slot * kMaxPipeline + k] == 0) gdone[k] = true;
                     }
                 }

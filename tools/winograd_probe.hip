@@ -107,6 +107,7 @@ extern "C" __global__ __launch_bounds__(512) void k_wino_probe(const uint16_t* _
             for (int xi = 0; xi < 16; ++xi) acc[b][xi] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
         for (int cb = 0; cb < 4; ++cb) {
             barrier();  // V is free, S holds the layer input
+#ifndef WP_SKIP_TRANSFORM  // attribution builds: MFMAs on stale V
             {
                 // d: 4 x 4 inputs of the tile (2 channels packed), zero outside the board
                 float d0[4][4], d1[4][4];
@@ -146,6 +147,7 @@ extern "C" __global__ __launch_bounds__(512) void k_wino_probe(const uint16_t* _
                     *reinterpret_cast<uint32_t*>(vb + (4 * i + 3) * 16 * kVRow) = pack2(a3, c3);
                 }
             }
+#endif
             barrier();  // V ready
 #pragma unroll
             for (int xi = 0; xi < 16; ++xi) {
@@ -160,6 +162,17 @@ extern "C" __global__ __launch_bounds__(512) void k_wino_probe(const uint16_t* _
             }
         }
         // epilogue: Y = A^T M A in-lane, + bias (+ skip on odd layers), ReLU, in place
+#ifdef WP_SKIP_EPILOGUE  // attribution builds: one store per board keeps the MFMAs live
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) {
+            f32x4_t s = acc[b][0];
+#pragma unroll
+            for (int xi = 1; xi < 16; ++xi) s += acc[b][xi];
+            *reinterpret_cast<u32x2_t*>(S + (b * 64 + tile) * kSRow + ob * 16 + kg * 4) =
+                (u32x2_t){pack2_relu(s[0], s[1]), pack2_relu(s[2], s[3])};
+        }
+        continue;
+#endif
         const bool second = (layer & 1) != 0;
         const float* bl = bias + (size_t)layer * kC + ob * 16 + kg * 4;
         const float bi[4] = {bl[0], bl[1], bl[2], bl[3]};
