@@ -26,6 +26,11 @@
 #                                  (summary: tools/record_summary.py)
 #   benchpmc NAME                  the four PMC passes over the C2 bench (tools/prof_summary.py bench)
 #   nnpmcset NAME [VAR=val ...]    the four PMC passes over the standalone kernel (tools/prof_summary.py nn)
+#   hostcpu NAME                   host CPU per rank: tools/host_threads.py and 2 interleaved short bench
+#                                  lines, poll-and-sleep waits vs OAMD_SPIN_SYNC=1 --spin-sync, then the
+#                                  world-2 gloo rehearsal on the one GPU (round 6)
+#   winoprobe NAME                 the Winograd tower probe and its attribution builds vs NativeNet
+#                                  (tools/winograd_probe.py; build: tools/winograd_probe_build.sh)
 # A/B sweeps are plain recipe lists, e.g. ROUNDS of
 #   bash tools/gpu.sh "bench a_1 ARGS_A" "bench b_1 ARGS_B" "bench a_2 ARGS_A" "bench b_2 ARGS_B"
 # (the round-4 one-off sweep scripts were folded into this form; their results are in profiles/r04/ab/).
@@ -129,6 +134,18 @@ run_recipe() {
       run_recipe nnpmc ${p}_a SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_WAIT_INST_LDS,SQ_INSTS_MFMA,SQ_INSTS_LDS,SQ_INSTS_SALU "$@" &&
         run_recipe nnpmc ${p}_b SQ_VALU_MFMA_BUSY_CYCLES,SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_INSTS_VALU,GRBM_GUI_ACTIVE "$@" &&
         run_recipe nnpmc ${p}_c FETCH_SIZE "$@" && run_recipe nnpmc ${p}_d WRITE_SIZE,TCC_HIT_sum,TCC_MISS_sum "$@" ;;
+    hostcpu) local n=$1
+      local A="--steps 20 --warmup 5 --sustained-moves 0 --cpu-baseline-moves 0 --deep-tree-moves 0 --latency-moves 0 --no-config-records"
+      step 200 "$OUT/hostcpu_${n}_threads_poll.json" python tools/host_threads.py &&
+        step 200 "$OUT/hostcpu_${n}_threads_spin.json" env OAMD_SPIN_SYNC=1 python tools/host_threads.py --spin-sync || return 1
+      for r in 1 2; do
+        step 300 "$OUT/hostcpu_${n}_poll_$r.json" python bench.py $A &&
+          step 300 "$OUT/hostcpu_${n}_spin_$r.json" env OAMD_SPIN_SYNC=1 python bench.py $A --spin-sync || return 1
+      done
+      step 600 "$OUT/hostcpu_${n}_rehearsal_world2_gloo.json" env OAMD_BENCH_BACKEND=gloo python bench.py --gpus 2 $A ;;
+    winoprobe) local n=$1 P=tools/_build
+      step 300 "$OUT/winoprobe_$n.json" python tools/winograd_probe.py $P/libwinoprobe_q4.so $P/libwinoprobe_noT.so \
+        $P/libwinoprobe_noE.so $P/libwinoprobe_noTE.so ;;
     *) echo "unknown recipe: $recipe"; return 2 ;;
   esac
 }
