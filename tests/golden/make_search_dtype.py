@@ -32,8 +32,17 @@ Nets: "selfplay" (bench_nets/selfplay_128x10b_h8, the trained net),
 "live256" (configs[3]'s net, 256x20b, first N256 positions only: 8x the CPU
 cost per evaluation).
 
-Runs in this container only (CPU; ~15 min with 8 threads). Imports nothing
+Case "selfplay_t2": the trained net under the self-play settings the bench
+runs (T = 2 x B = 16, eps = 0.25 Dirichlet noise drawn from the same key
+streams, train.py:250's MCTS config), first N_T2 positions. The engine
+computes the reference's thread interleaving deterministically (DESIGN.md
+§2), so with the same key the only difference left is the NN precision;
+under the other key the noise vectors differ too.
+
+Runs in this container only (CPU; ~25 min with 8 threads). Imports nothing
 from the reference. Usage: python tests/golden/make_search_dtype.py
+[--only CASE ...] (recompute those cases, keep the others of the committed
+fixture)
 """
 
 from __future__ import annotations
@@ -61,6 +70,7 @@ THREADS = 1
 BATCH = 16
 N = 128
 N256 = 48
+N_T2 = 64
 SEEDS = (0x5EA4C4A1, 0x5EA4C4B2)  # engine seeds of key streams A and B
 M64 = (1 << 64) - 1
 
@@ -72,11 +82,14 @@ def game_key(seed: int, g: int) -> int:
 
 
 def nets() -> dict:
+    """case -> (state_dict, positions, (num_threads, batch_size, dirichlet_epsilon))."""
     from othello_mcts.synthetic import live_state_dict, selfplay_state_dict
 
-    return {"selfplay": (selfplay_state_dict(), N),
-            "live128": (live_state_dict(2025, 17, 128, 9, 128), N),
-            "live256": (live_state_dict(2025, 17, 256, 19, 256), N256)}
+    base = (THREADS, BATCH, 0.0)
+    return {"selfplay": (selfplay_state_dict(), N, base),
+            "live128": (live_state_dict(2025, 17, 128, 9, 128), N, base),
+            "live256": (live_state_dict(2025, 17, 256, 19, 256), N256, base),
+            "selfplay_t2": (selfplay_state_dict(), N_T2, (2, 16, 0.25))}
 
 
 def torch_sd(sd):
@@ -117,8 +130,9 @@ def replay(actions_row) -> list[int]:
     return [a for a in actions_row if a >= 0]
 
 
-def search_all(sd, actions: np.ndarray, n: int, seed: int) -> tuple[np.ndarray, np.ndarray]:
+def search_all(sd, actions: np.ndarray, n: int, seed: int, params=(THREADS, BATCH, 0.0)) -> tuple[np.ndarray, np.ndarray]:
     """Root visit counts and Q (n, 65), indexed by action, fp32 oracle search."""
+    threads, batch, eps = params
     sdt = torch_sd(sd)
 
     def nn(feat):
@@ -129,12 +143,13 @@ def search_all(sd, actions: np.ndarray, n: int, seed: int) -> tuple[np.ndarray, 
     visits = np.zeros((n, 65), np.int32)
     q = np.zeros((n, 65), np.float32)
     for g in range(n):
-        m = O.OracleMCTS(history_size=H, num_simulations=SIMS, num_threads=THREADS, batch_size=BATCH,
-                         dirichlet_epsilon=0.0, game_key=game_key(seed, g))
+        m = O.OracleMCTS(history_size=H, num_simulations=SIMS, num_threads=threads, batch_size=batch,
+                         dirichlet_epsilon=eps, game_key=game_key(seed, g))
         for a in replay(actions[g]):
             m.apply_action(int(a))
         sims = m.search(nn)
-        assert sims == SIMS
+        L = threads * batch
+        assert sims == L * ((SIMS + L - 1) // L)
         legal = O.legal_actions(m.position())
         visits[g, legal] = m.visit_counts()
         q[g, legal] = m.mean_action_values()
@@ -151,6 +166,11 @@ def summary(va: np.ndarray, vb: np.ndarray) -> dict:
 
 
 def main() -> None:
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None)
+    only = ap.parse_args().only
     torch.set_num_threads(8)
     allnets = nets()
     t0 = time.time()
@@ -161,15 +181,24 @@ def main() -> None:
             "positions": N, "plies": [int((r >= 0).sum()) for r in actions],
             "game_keys": {str(s): [str(game_key(s, g)) for g in range(N)] for s in SEEDS},
             "nets": {}, "generator": "tests/golden/make_search_dtype.py"}
-    for name, (sd, n) in allnets.items():
+    if only:  # keep the committed cases, recompute the named ones
+        old = json.loads((GOLD / "search_dtype.json").read_text())
+        old_arr = dict(np.load(GOLD / "search_dtype.npz", allow_pickle=False))
+        assert np.array_equal(old_arr["actions"], actions)
+        arrays.update(old_arr)
+        meta["nets"].update(old["nets"])
+    for name, (sd, n, params) in allnets.items():
+        if only and name not in only:
+            continue
         res = []
         for s in SEEDS:
-            v, q = search_all(sd, actions, n, s)
+            v, q = search_all(sd, actions, n, s, params)
             arrays[f"{name}_visits_{s:x}"] = v
             arrays[f"{name}_q_{s:x}"] = q
             res.append(v)
             print(f"{name} seed {s:x}: {time.time() - t0:.0f} s", flush=True)
-        meta["nets"][name] = {"positions": n, "fp32_key_a_vs_key_b": summary(*res)}
+        meta["nets"][name] = {"positions": n, "num_threads": params[0], "batch_size": params[1],
+                              "dirichlet_epsilon": params[2], "fp32_key_a_vs_key_b": summary(*res)}
         print(name, meta["nets"][name], flush=True)
     np.savez_compressed(GOLD / "search_dtype.npz", **arrays)
     (GOLD / "search_dtype.json").write_text(json.dumps(meta, indent=1) + "\n")

@@ -58,20 +58,22 @@ def _fixture(golden_dir):
 def _state_dict(name):
     from othello_mcts.synthetic import live_state_dict, selfplay_state_dict
 
-    if name == "selfplay":
+    if name.startswith("selfplay"):
         return selfplay_state_dict()
     if name == "live128":
         return live_state_dict(2025, 17, 128, 9, 128)
     return live_state_dict(2025, 17, 256, 19, 256)
 
 
-def _search(om, meta, actions, n, seed, net):
+def _search(om, meta, case, actions, n, seed, net):
     """The fixture's searches on the engine: n games replay their actions from
-    the initial position (history kept), then one search each."""
+    the initial position (history kept), then one search each (the case's
+    threads, batch size and Dirichlet epsilon)."""
+    c = meta["nets"][case]
+    T, B = c.get("num_threads", meta["num_threads"]), c.get("batch_size", meta["batch_size"])
     b = om.BatchedMCTS(n, history_size=meta["history_size"], num_simulations=meta["num_simulations"],
-                       num_threads=meta["num_threads"], batch_size=meta["batch_size"],
-                       dirichlet_epsilon=meta["dirichlet_epsilon"], c_puct_base=meta["c_puct_base"],
-                       c_puct_init=meta["c_puct_init"], seed=seed)
+                       num_threads=T, batch_size=B, dirichlet_epsilon=c.get("dirichlet_epsilon", meta["dirichlet_epsilon"]),
+                       c_puct_base=meta["c_puct_base"], c_puct_init=meta["c_puct_init"], seed=seed)
     keys = meta["game_keys"][str(seed)]
     assert all(b.engine.game_key(g) == int(keys[g]) for g in range(n))
     dev = b.device
@@ -80,7 +82,8 @@ def _search(om, meta, actions, n, seed, net):
         if (col >= 0).any():
             b.apply_actions(col)
     sims, _ = b.search(net)
-    assert sims == n * meta["num_simulations"]
+    L = T * B
+    assert sims == n * L * ((meta["num_simulations"] + L - 1) // L)
     assert b.engine.status() == (0, 0)
     v, _ = b.root_stats()
     return v.cpu().numpy()
@@ -115,10 +118,12 @@ BOUNDS = {
     ("live128", "fp16"): (0.30, 0.46),
     ("live256", "bf16"): (0.25, 0.58),
     ("live256", "fp16"): (0.30, 0.52),
+    ("selfplay_t2", "bf16"): (0.0, 1.0),  # set from the first measurement
+    ("selfplay_t2", "fp16"): (0.0, 1.0),
 }
 
 
-@pytest.mark.parametrize("name", ["selfplay", "live128", "live256"])
+@pytest.mark.parametrize("name", ["selfplay", "live128", "live256", "selfplay_t2"])
 def test_native_search_agrees_with_fp32_search(golden_dir, name):
     import othello_mcts as om
 
@@ -133,14 +138,14 @@ def test_native_search_agrees_with_fp32_search(golden_dir, name):
     sd = _state_dict(name)
     # wiring: the engine with the fp32 restatement on the GPU
     sdt = {k: torch.from_numpy(np.asarray(v)).to("cuda:0") for k, v in sd.items()}
-    fp32 = compare(_search(om, meta, actions, n, seed_a, lambda f: resnet_ref.forward(sdt, f)), fa)
+    fp32 = compare(_search(om, meta, name, actions, n, seed_a, lambda f: resnet_ref.forward(sdt, f)), fa)
     numerics.record(f"search dtype {name}: engine + fp32 resnet_ref (GPU) vs fixture", _fmt(fp32))
     res = {}
     for dtype in ("bf16", "fp16"):
         net = om.NativeNet(sd, device=0, dtype=dtype)
-        c = compare(_search(om, meta, actions, n, seed_a, net), fa)
+        c = compare(_search(om, meta, name, actions, n, seed_a, net), fa)
         # the same net under key B: the native search against the other stream too
-        cb = compare(_search(om, meta, actions, n, seed_b, net), fb)
+        cb = compare(_search(om, meta, name, actions, n, seed_b, net), fb)
         res[dtype] = (c, cb)
         numerics.record(f"search dtype {name}: native {dtype} vs fp32, same keys",
                         f"key A {_fmt(c)}; key B {_fmt(cb)}")
