@@ -192,3 +192,39 @@ def test_sustained_record_uses_its_own_moves():
     assert out["work"]["rows_launched"] == 256 * 800 * 64
     assert out["work"]["terminal_share"] == pytest.approx(0.15, abs=1e-3)
     assert out["roofline"]["timed_region_launches"] == 64 * 2 * 33
+
+
+def test_byte_models():
+    """Round 6: the tree kernels' algorithmic bytes are
+    SURVEY §8(d)'s per-item constants over the engine's counters, per tree
+    launch; the ResNet's are the weights once + 408 B per evaluated row; each
+    line's counter traffic is divided by them."""
+    args = bench.parse_args([])
+    m = _m()
+    tw = {"levels": 1000, "children_scanned": 9000, "expansions": 300, "children_created": 3000, "launches": 10}
+    m["tree_work"] = tw
+    out = bench.measured_fields(args, m, "w")
+    t = out["tree_kernels"]["k_tree"]
+    per_row = 8 * 16 + 17 * 8 + 65 * 2 + 2
+    expect = 12 * 9000 + 32 * 1000 + 8 * 300 + 28 * 3000 + per_row * m["evals"]
+    assert bench.tree_bytes_per_row(8) == per_row == 396
+    assert t["algorithmic_bytes_per_launch"] == round(expect / 10)
+    assert t["algorithmic_bytes_per_sim"] == pytest.approx(expect / m["sims"], abs=0.1)
+    assert t["byte_model"]["children_scanned_per_level"] == 9.0
+    assert t["byte_model"]["children_per_expansion"] == 10.0
+    # 128x10b, H=8: 19 3x3 convs in bf16 (5.35 MB) + fp32 biases and heads
+    wb = bench.resnet_weight_bytes(17, 128, 9, 128)
+    convs = 9 * 17 * 128 + 18 * 9 * 128 * 128
+    assert wb == 2 * convs + 4 * (19 * 128 + 387 + 8385 + 8320 + 129)
+    r = out["roofline"]
+    n_eval = m["evals"] / m["busy_launches"]
+    assert r["algorithmic_bytes_per_launch"] == round(wb + 408 * n_eval)
+    assert bench.RESNET_ROW_BYTES == 408
+
+
+def test_host_budget():
+    ranks = [{"rank": 0, "cpu_s_per_s": 0.08}, {"rank": 1, "cpu_s_per_s": 0.1}]
+    h = bench.host_budget(ranks)
+    assert h["ranks"] == 2 and h["cpu_s_per_s_max"] == 0.1 and h["cpu_s_per_s_sum"] == 0.18
+    assert h["need_at_8_ranks"] == 0.8 and h["fits_8_ranks"] is (0.8 <= h["usable_cpus"])
+    assert "cpu_s_per_s_max" not in bench.host_budget([{"rank": 0}])
