@@ -5,9 +5,11 @@ one game with the fused native ResNet, as ``player.py``/``train.py`` use it.
 Prints one JSON line per setting: median / p90 ms per ``search`` over the
 moves of one game (argmax play), for self-play settings (800 sims, T=2 x B=16,
 eps=0.25) and evaluation settings (3200 sims, eps=0, README.md:195).
-Seeded live 128x10b weights (the bench's)."""
+Seeded live 128x10b weights (the bench's). LAT_DTYPE=fp16 (default bf16):
+the NativeNet the drop-in MCTS converts a module to since round 6."""
 
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -73,7 +75,8 @@ def breakdown(net, sims, moves, eps=0.25):
 
 
 def main():
-    net = om.NativeNet(live_state_dict(2025, 17, 128, 9, 128), device=0)
+    net = om.NativeNet(live_state_dict(2025, 17, 128, 9, 128), device=0, dtype=os.environ.get("LAT_DTYPE", "bf16"))
+    print(json.dumps({"dtype": net.dtype}), flush=True)
     for sims, eps, moves in ((800, 0.25, 40), (3200, 0.0, 20)):
         print(json.dumps(run(net, sims, eps, moves)), flush=True)
     print(json.dumps(breakdown(net, 800, 20)), flush=True)
