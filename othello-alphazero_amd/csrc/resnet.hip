@@ -118,6 +118,25 @@ __host__ __device__ constexpr int wide_dy(int J) { return J % 3 - 1; }
 // window rows (bit i = board row i - 1) K-step J needs first: rows 0-6 at
 // dy = -1, row 7 at dy = 0
 __host__ __device__ constexpr int wide_new(int J) { return J % 3 == 0 ? 0xFE : (J % 3 == 1 ? 0x100 : 0); }
+// Epilogue without its first barrier (OAMD_EPI_NOBAR, round 6; tower layers
+// of the C=128 edge-row geometry, which has a weight ring): the layer's last
+// (dx, block) reads its whole window, rows 0-7, at its first K-step, so every
+// activation read of the layer is issued before the barrier that opens the
+// layer's last stage; after it no wave reads the layer's input, and a wave
+// overwrites its outputs in place as soon as its own MFMAs are done (the
+// wait at the first barrier was 1.5 % of the tower's cycles).
+// The last stage's weight slot is refilled after the second (post-store)
+// barrier instead. Same box, 4096 rows, interleaved, bit-identical:
+// 0.787-0.796 vs 0.796-0.808 ms. Not for the register-queue geometry
+// (C=256, DIRECT): it has no stage barriers, so nothing orders the other
+// waves' last reads before a store (its outputs differed when tried).
+#ifndef OAMD_EPI_NOBAR
+#define OAMD_EPI_NOBAR 1
+#endif
+template <bool ENABLE>
+__host__ __device__ constexpr int wide_new_last(int J, int NJ) {
+    return !ENABLE || J < NJ - 3 ? wide_new(J) : (J % 3 == 0 ? 0x1FE : 0);
+}
 
 // Head parameter buffer layout (fp32), filled by oamd_net_load_state (capi.hip).
 struct HeadLayout {
@@ -1071,11 +1090,15 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
             // read the zero border: left out, every wave alike); reads the
             // window rows K-step J + 1 needs (at sbn: the next dx's base when
             // J = NJ - 1) and its weights
-            auto wstep = [&](auto JJ, const Frags<kNT, kMT>& wc, Frags<kNT, kMT>& wn, int sbn) {
+            auto wstep = [&](auto JJ, auto LASTDX, const Frags<kNT, kMT>& wc, Frags<kNT, kMT>& wn, int sbn) {
                 constexpr int J = decltype(JJ)::value;
                 constexpr int Jn = (J + 1) % NJ;
                 constexpr bool open = Jn % G::KS == 0 && !G::DIRECT;
-                constexpr int dy = wide_dy(J), cbn = wide_cb(Jn), nnew = __builtin_popcount(wide_new(Jn));
+                // rows of the window K-step Jn needs first (the layer's last dx:
+                // wide_new_last, OAMD_EPI_NOBAR)
+                constexpr int newmask =
+                    decltype(LASTDX)::value ? wide_new_last<OAMD_EPI_NOBAR && !G::DIRECT>(Jn, NJ) : wide_new(Jn);
+                constexpr int dy = wide_dy(J), cbn = wide_cb(Jn), nnew = __builtin_popcount(newmask);
                 constexpr int mlo = dy < 0 ? 1 : 0, mhi = dy > 0 ? 7 : 8;
                 auto& Wc = [&]() -> u32x4_t(&)[9] {
                     if constexpr (wide_cb(J) % 2 == 0) return win0; else return win1;
@@ -1087,7 +1110,7 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 OAMD_STEP_WAIT(__builtin_amdgcn_s_waitcnt(0xC07F));  // lgkmcnt(0): wc / Wc have landed
                 static_for<9>([&](auto I) {
                     constexpr int i = decltype(I)::value;
-                    if constexpr ((wide_new(Jn) >> i) & 1)
+                    if constexpr ((newmask >> i) & 1)
                         Wn[i] = *reinterpret_cast<const u32x4_t*>(act + sbn + i * RS + cbn * 64);
                 });
                 if constexpr (open) {
@@ -1124,8 +1147,8 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
                 static_for<lastdx ? NJ - 1 : NJ>([&](auto JJ) {
                     constexpr int J = decltype(JJ)::value;
                     const int sbn = J == NJ - 1 ? sb + G::RP : sb;
-                    if constexpr (J % 2 == 0) wstep(JJ, fa, fb, sbn);
-                    else wstep(JJ, fb, fa, sbn);
+                    if constexpr (J % 2 == 0) wstep(JJ, LASTDX, fa, fb, sbn);
+                    else wstep(JJ, LASTDX, fb, fa, sbn);
                 });
                 if constexpr (lastdx) {
                     // the layer's last K-step = (last block, dy +1) in fb / win1
@@ -1176,9 +1199,16 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         pw_on = false;
 #endif
         OAMD_EP_MARK(0);
-        lds_barrier();  // every wave is done reading this layer's input and its last stage
+        // OAMD_EPI_NOBAR: no wave reads this layer's input after the barrier that
+        // opened its last stage (wide_new_last), so the stores need no barrier;
+        // the last stage's slot is refilled after the post-store barrier
+        constexpr bool nobar = OAMD_EPI_NOBAR && kWide && !first && !G::DIRECT;
+        const int last_slot = slot;  // the slot of the layer's last stage
+        if constexpr (!nobar) {
+            lds_barrier();  // every wave is done reading this layer's input and its last stage
+        }
         OAMD_EP_MARK(1);
-        if constexpr (!G::DIRECT) {
+        if constexpr (!G::DIRECT && !nobar) {
             wcur += G::STAGE;
             issue_stage_dma<G, G::OPEN_PART>(wcur, ring, (slot + G::AHEAD + 1) % G::RING, tid);
         }
@@ -1212,9 +1242,15 @@ __device__ __forceinline__ void resnet_body(NetView N, const void* __restrict__ 
         slot = slot == G::RING - 1 ? 0 : slot + 1;
         OAMD_EP_MARK(2);
         if (more) {
-            // the next layer's first stage has landed (later may fly)
-            if constexpr (!G::DIRECT) wait_vm<G::VM_LAYER>();
+            // the next layer's first stage has landed (later may fly; with
+            // nobar the epilogue's DMA is not issued yet: one fewer in flight)
+            if constexpr (!G::DIRECT) wait_vm<nobar ? G::VM_LAYER - 1 : G::VM_LAYER>();
             lds_barrier();  // ... and this layer's output is complete
+            if constexpr (!G::DIRECT && nobar) {
+                // every wave is past its last K-step: the last stage's slot is free
+                wcur += G::STAGE;
+                issue_stage_dma<G, G::OPEN_PART>(wcur, ring, (last_slot + G::AHEAD + 1) % G::RING, tid);
+            }
             if constexpr (kWide) {
                 if constexpr (!G::DIRECT) load_wfrags(fa, ring + slot * G::STAGE, wl);
 #pragma unroll
