@@ -40,7 +40,7 @@ template <int MODE>
 __global__ __launch_bounds__(512) void k_mfma_loop(const u32x4_t* __restrict__ src, float* __restrict__ out) {
     __shared__ u32x4_t lds[8 * 512];  // 64 KiB: 8 B fragments per wave slot
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const u32x4_t* s = src + ((size_t)blockIdx.x * 512 + tid) * 10 % (1 << 20);
+    const u32x4_t* s = src + ((size_t)blockIdx.x * 512 + tid) * 10 % ((1 << 20) - 16);  // + 10 fragments stay inside
     u32x4_t a[2], b[8];
     for (int i = 0; i < 2; ++i) a[i] = s[i];
     for (int i = 0; i < 8; ++i) b[i] = s[2 + i];
