@@ -949,6 +949,21 @@ def traffic_record(name: str, kind: str, workload: str) -> dict | None:
     return tj
 
 
+def mfma_ceiling(dtype: str) -> dict | None:
+    """The bf16 MFMA rate this chip sustains on random operands at the clock
+    it holds under load (committed probe record profiles/mfma_ceiling.json,
+    tools/mfma_ceiling.hip: k_resnet_w8's wave tile, operands in registers),
+    to read the spec-peak `frac` against. bf16 only (the probe's dtype)."""
+    f = ROOT / "profiles" / "mfma_ceiling.json"
+    if dtype != "bf16" or not f.exists():
+        return None
+    try:
+        c = json.loads(f.read_text())
+        return {"TFLOP_s": float(c["ceiling_TFLOP_s"]), "tag": c.get("tag"), "source": "profiles/mfma_ceiling.json"}
+    except (ValueError, OSError, KeyError, TypeError):
+        return None
+
+
 def measured_fields(args, m: dict, workload: str) -> dict:
     """roofline (the fused ResNet kernel), tree-kernel timings and the work
     counters of this rank's timed region."""
@@ -1026,6 +1041,12 @@ def measured_fields(args, m: dict, workload: str) -> dict:
             if "algorithmic_bytes_per_launch" in entry:
                 entry["counter_over_algorithmic"] = round(tree_bytes[name] / max(1.0, alg_tree["per_launch"]), 3)
         tree[name] = entry
+    executed_tfs = executed * n_eval_per_launch / (busy_ms * 1e-3) / 1e12
+    ceiling = mfma_ceiling(args.dtype)
+    if ceiling:
+        # algorithmic and executed rates against the measured random-data ceiling
+        ceiling.update({"frac_achieved": round(achieved / ceiling["TFLOP_s"], 4),
+                        "frac_executed": round(executed_tfs / ceiling["TFLOP_s"], 4)})
     return {
         "overflow_games": m["overflow_games"],
         "work": {"simulations": m["sims"], "n_eval": m["evals"], "rows_launched": rows_launched,
@@ -1062,7 +1083,8 @@ def measured_fields(args, m: dict, workload: str) -> dict:
             # all zero border (1/12 of every tower conv): achieved
             # counts the algorithmic FLOPs above, these are the ones executed
             "executed_flops_per_row": executed,
-            "executed_TFLOP_s": round(executed * n_eval_per_launch / (busy_ms * 1e-3) / 1e12, 2),
+            "executed_TFLOP_s": round(executed_tfs, 2),
+            "measured_ceiling": ceiling,
         },
         "tree_kernels": tree,
     }

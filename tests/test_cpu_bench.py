@@ -228,3 +228,17 @@ def test_host_budget():
     assert h["ranks"] == 2 and h["cpu_s_per_s_max"] == 0.1 and h["cpu_s_per_s_sum"] == 0.18
     assert h["need_at_8_ranks"] == 0.8 and h["fits_8_ranks"] is (0.8 <= h["usable_cpus"])
     assert "cpu_s_per_s_max" not in bench.host_budget([{"rank": 0}])
+
+
+def test_measured_ceiling_in_roofline():
+    """The committed random-data MFMA ceiling (tools/mfma_ceiling.hip) is read
+    into the bf16 roofline next to the spec-peak frac; fp16 has no record."""
+    c = bench.mfma_ceiling("bf16")
+    assert c is not None and 1000.0 < c["TFLOP_s"] <= 2500.0
+    assert bench.mfma_ceiling("fp16") is None
+    args = bench.parse_args([])
+    r = bench.measured_fields(args, _m(), "w")["roofline"]
+    mc = r["measured_ceiling"]
+    assert mc["frac_achieved"] == pytest.approx(r["achieved"] / c["TFLOP_s"], abs=1e-3)
+    assert mc["frac_executed"] == pytest.approx(r["executed_TFLOP_s"] / c["TFLOP_s"], abs=1e-3)
+    assert r["frac"] == pytest.approx(r["achieved"] / 2500.0, abs=1e-4)  # the line's frac stays on the spec peak
