@@ -407,6 +407,9 @@ def parse_args(argv: list[str]):
                     help="workgroups of the extra rounds' ResNet launches (0 = the regular grid)")
     ap.add_argument("--cpu-baseline-moves", type=int, default=24,
                     help="timed moves of the CPU baseline (0 = skip it), after 2 warm-up moves")
+    ap.add_argument("--no-ceiling-probe", dest="ceiling_probe", action="store_false",
+                    help="skip the same-box MFMA ceiling probe after the timed regions (roofline.measured_ceiling "
+                         "then comes from the committed record)")
     ap.add_argument("--cpu-baseline-threads", type=int, default=0,
                     help="torch threads of the CPU baseline (0 = every CPU this process may use)")
     ap.add_argument("--sustained-moves", type=int, default=64,
@@ -763,6 +766,14 @@ def report(args, world: int, rank: int, backend: str, wl) -> None:
             result["other_configs"] = config_records(args, wl, world, rank, backend)
         if args.latency_moves > 0 and rank == 0:
             result["latency"] = latency_record(args, wl)
+    # the MFMA ceiling on this box (rank 0's GPU), after every timed region
+    if m is not None and rank == 0 and args.ceiling_probe:
+        rl = [(args.dtype, result["roofline"])] + [(v.get("dtype"), v["roofline"])
+                                                   for v in result.get("other_configs", {}).values()]
+        got = same_box_ceiling({d for d, _ in rl})
+        for d, r in rl:
+            if d in got:
+                with_ceiling(r, got[d], "this box: tools/mfma_ceiling.hip after the timed regions")
     # the CPU baseline on rank 0 at every world size, after every timed region;
     # the other ranks wait at a gloo barrier (blocked, not spinning)
     if args.cpu_baseline_moves > 0 and (m is not None or args.dry_run):
@@ -871,7 +882,8 @@ def config_records(args, wl, world: int, rank: int, backend: str) -> dict:
                      "dtype": a.dtype,
                      "roofline": {k: r[k] for k in ("bound", "achieved", "peak", "unit", "frac", "busy_ms_per_launch",
                                                     "rows_per_launch", "n_eval_per_launch", "flops_per_row",
-                                                    "timed_region_launches")},
+                                                    "timed_region_launches", "executed_TFLOP_s",
+                                                    "measured_ceiling")},
                      "work": mf["work"], "tree_kernels": mf["tree_kernels"]}
         del w
         gc.collect()
@@ -949,19 +961,59 @@ def traffic_record(name: str, kind: str, workload: str) -> dict | None:
     return tj
 
 
+CEILING_PROBES = {"bf16": "regs_random", "fp16": "f16_regs_random"}
+
+
 def mfma_ceiling(dtype: str) -> dict | None:
-    """The bf16 MFMA rate this chip sustains on random operands at the clock
-    it holds under load (committed probe record profiles/mfma_ceiling.json,
-    tools/mfma_ceiling.hip: k_resnet_w8's wave tile, operands in registers),
-    to read the spec-peak `frac` against. bf16 only (the probe's dtype)."""
+    """The MFMA rate this chip sustains on random operands at the clock it
+    holds under load (tools/mfma_ceiling.hip: k_resnet_w8's wave tile, operands
+    in registers), to read the spec-peak `frac` against: the committed probe
+    record (profiles/mfma_ceiling.json); report() replaces it with this box's
+    own probe run after the timed regions (same_box_ceiling)."""
     f = ROOT / "profiles" / "mfma_ceiling.json"
-    if dtype != "bf16" or not f.exists():
+    if dtype not in CEILING_PROBES or not f.exists():
         return None
     try:
         c = json.loads(f.read_text())
-        return {"TFLOP_s": float(c["ceiling_TFLOP_s"]), "tag": c.get("tag"), "source": "profiles/mfma_ceiling.json"}
+        tfs = c["probes"][CEILING_PROBES[dtype]]["TFLOP_s"]
+        return {"TFLOP_s": float(tfs), "tag": c.get("tag"), "source": "profiles/mfma_ceiling.json (another box)"}
     except (ValueError, OSError, KeyError, TypeError):
         return None
+
+
+def same_box_ceiling(dtypes) -> dict:
+    """{dtype: TFLOP/s} from tools/_build/mfma_ceiling (built by
+    __graft_entry__.build()) run as a child process on this rank's GPU after
+    every timed region; {} if the probe is missing or fails (the lines then
+    keep the committed record)."""
+    exe = ROOT / "tools" / "_build" / "mfma_ceiling"
+    names = {CEILING_PROBES[d]: d for d in dtypes if d in CEILING_PROBES}
+    if not names or not exe.exists():
+        return {}
+    try:
+        r = subprocess.run([str(exe), ",".join(names)], capture_output=True, text=True, timeout=120)
+    except (OSError, subprocess.TimeoutExpired):
+        return {}
+    out = {}
+    for ln in r.stdout.splitlines():
+        try:
+            j = json.loads(ln)
+        except ValueError:
+            continue
+        if j.get("probe") in names:
+            out[names[j["probe"]]] = float(j["TFLOP_s"])
+    return out
+
+
+def with_ceiling(roofline: dict, tfs: float, source: str) -> None:
+    """roofline.measured_ceiling = `tfs`, with the achieved (algorithmic) and
+    executed rates as fractions of it."""
+    c = {"TFLOP_s": round(tfs, 1), "source": source}
+    if "achieved" in roofline:
+        c["frac_achieved"] = round(roofline["achieved"] / tfs, 4)
+    if "executed_TFLOP_s" in roofline:
+        c["frac_executed"] = round(roofline["executed_TFLOP_s"] / tfs, 4)
+    roofline["measured_ceiling"] = c
 
 
 def measured_fields(args, m: dict, workload: str) -> dict:

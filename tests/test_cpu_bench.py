@@ -232,13 +232,34 @@ def test_host_budget():
 
 def test_measured_ceiling_in_roofline():
     """The committed random-data MFMA ceiling (tools/mfma_ceiling.hip) is read
-    into the bf16 roofline next to the spec-peak frac; fp16 has no record."""
+    into the roofline next to the spec-peak frac."""
     c = bench.mfma_ceiling("bf16")
     assert c is not None and 1000.0 < c["TFLOP_s"] <= 2500.0
-    assert bench.mfma_ceiling("fp16") is None
+    assert bench.mfma_ceiling("fp16") is not None and bench.mfma_ceiling("fp32") is None
     args = bench.parse_args([])
     r = bench.measured_fields(args, _m(), "w")["roofline"]
     mc = r["measured_ceiling"]
     assert mc["frac_achieved"] == pytest.approx(r["achieved"] / c["TFLOP_s"], abs=1e-3)
     assert mc["frac_executed"] == pytest.approx(r["executed_TFLOP_s"] / c["TFLOP_s"], abs=1e-3)
     assert r["frac"] == pytest.approx(r["achieved"] / 2500.0, abs=1e-4)  # the line's frac stays on the spec peak
+
+
+def test_same_box_ceiling_parses_the_probe(tmp_path, monkeypatch):
+    """same_box_ceiling runs tools/_build/mfma_ceiling with the dtypes' probe
+    names and maps its JSON lines back to dtypes; with_ceiling puts the rate
+    and both fractions into a roofline; a missing probe gives {}."""
+    exe = tmp_path / "tools" / "_build" / "mfma_ceiling"
+    exe.parent.mkdir(parents=True)
+    exe.write_text("#!/bin/sh\n"
+                   "echo \"args=$1\"\n"
+                   "echo '{\"probe\": \"regs_random\", \"TFLOP_s\": 2000.0}'\n"
+                   "echo '{\"probe\": \"f16_regs_random\", \"TFLOP_s\": 1900.0}'\n")
+    exe.chmod(0o755)
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    assert bench.same_box_ceiling({"bf16", "fp16"}) == {"bf16": 2000.0, "fp16": 1900.0}
+    assert bench.same_box_ceiling({"fp32"}) == {}
+    r = {"achieved": 1800.0, "executed_TFLOP_s": 1650.0}
+    bench.with_ceiling(r, 2000.0, "test")
+    assert r["measured_ceiling"] == {"TFLOP_s": 2000.0, "source": "test", "frac_achieved": 0.9, "frac_executed": 0.825}
+    exe.unlink()
+    assert bench.same_box_ceiling({"bf16"}) == {}

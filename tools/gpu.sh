@@ -105,7 +105,7 @@ run_recipe() {
         for v in ${AB_ORDER:-$(ls abv)}; do
           cp abv/$v/liboamd.so $PKG/liboamd.so
           step 600 "$OUT/benchvar_${n}_${v}_$r.json" env OAMD_AB_VARIANT=$v python bench.py --cpu-baseline-moves 0 \
-            --deep-tree-moves 0 --latency-moves 0 --no-config-records "$@" || { restore_lib; return 1; }
+            --deep-tree-moves 0 --latency-moves 0 --no-config-records --no-ceiling-probe "$@" || { restore_lib; return 1; }
         done
       done
       restore_lib ;;
@@ -121,7 +121,7 @@ run_recipe() {
     records)
       local C2="--steps 20 --warmup 5" C4="--sims 1600 --channels 256 --blocks 20 --hidden 256 --steps 4 --warmup 1"
       local C5="--games 512 --dtype fp16 --eval-batch 2048 --steps 10 --warmup 2"
-      local Q="--sustained-moves 0 --cpu-baseline-moves 0 --deep-tree-moves 0 --latency-moves 0 --no-config-records"
+      local Q="--sustained-moves 0 --cpu-baseline-moves 0 --deep-tree-moves 0 --latency-moves 0 --no-config-records --no-ceiling-probe"
       run_recipe tests && run_recipe bench c2 $C2 && run_recipe trace c2 $C2 $Q &&
         run_recipe trace s200 --steps 200 --warmup 5 $Q && run_recipe trace c4 $C4 $Q &&
         run_recipe trace c5 $C5 $Q && run_recipe launch c2 $C2 $Q ;;
