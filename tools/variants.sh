@@ -13,7 +13,7 @@ set -eu
 cd "$(dirname "$0")/.."
 B=othello-alphazero_amd/build
 CS=othello-alphazero_amd/csrc
-RF="-mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp"
+RF=${RF-"-mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-ilp"}  # env RF overrides (scheduler A/Bs)
 CXX="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -fno-gpu-rdc"
 EXACT="-ffp-contract=off -fno-fast-math"
 NOSCALAR="-mllvm -amdgpu-scalarize-global-loads=false"  # as build.py builds tree.hip
